@@ -1,0 +1,253 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X LSD radix sort (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+A step is one full sort (mySort: 8 passes of 8-bit digits over 64-bit keys)
+of 2^30 16-byte records per GPU (weak scaling: n = N * 2^30), generated on
+device with the reference's PCG64 input (seed = rank, val = global index;
+mpi/mpi_lsbsort.cpp:650-656) before every step, outside the timed window —
+the reference times the sort only (mpi/mpi_lsbsort.cpp:688-699).  Each step
+is bracketed by a barrier + device synchronize on both sides; the time is
+the max over ranks.  The result of the last step is verified on device
+(bit-exact stable-sort invariant, lsb_verify).
+
+Multi-GPU: one process per GPU (RANK / WORLD_SIZE / LOCAL_RANK from the
+environment).  torch.distributed (gloo, CPU) only ships the RCCL unique id
+and reduces timings; the data path is the library's own RCCL communicator.
+
+The JSON line carries the roofline of the dominant kernel (k_scatter, 32
+algorithmic bytes per record per launch, timed with HIP events on the
+library's stream) and, on rank 0 at N = 1, a CPU baseline: the reference's
+own mpi_lsbsort (oracle/_ref, built from /root/reference) on the host cores.
+"""
+import argparse
+import json
+import os
+import re
+import shutil
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "distributed-lsb_amd"))
+
+import lsbsort  # noqa: E402
+
+METRIC = "Melem/s (16-byte elems) at 1/2/4/8 GPUs; per-pass HBM GB/s vs roofline"
+HBM_PEAK_GBS = 8000.0           # MI355X HBM3E spec (MI355X_MICROARCH.md)
+SCATTER_BYTES_PER_ELEM = 32     # 16 B read + 16 B written per record per pass
+PASS_BYTES_PER_ELEM = 48        # + 16 B histogram read
+REF_MPI_MELEMS = 830.0          # mpi_lsbsort, 64 nodes x 128 cores, n = 2^36
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--n-per-gpu", type=int, default=1 << 30)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=1 << 27,
+                    help="records the CPU baseline sorts (bounded sample)")
+    ap.add_argument("--no-verify", action="store_true")
+    return ap.parse_args()
+
+
+class Dist:
+    """Rank bookkeeping: torch.distributed (gloo) when WORLD_SIZE > 1."""
+
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", str(self.rank)))
+        self.dist = None
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
+            self.dist = dist
+
+    def bcast_bytes(self, b):
+        if not self.dist:
+            return b
+        obj = [b]
+        self.dist.broadcast_object_list(obj, src=0)
+        return obj[0]
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def max(self, x):
+        if not self.dist:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def all_true(self, ok):
+        if not self.dist:
+            return ok
+        import torch
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN)
+        return bool(t.item())
+
+    def close(self):
+        if self.dist:
+            self.dist.destroy_process_group()
+
+
+def device_sync():
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+    except Exception:
+        pass
+
+
+def load_traffic(workload):
+    """Per-launch HBM bytes of k_scatter from the committed rocprofv3 PMC summary."""
+    path = os.path.join(ROOT, "profiles", "pmc_scatter.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("workload") == workload:
+            return d.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def cpu_baseline(sample):
+    """The reference's own MPI sort on this host's cores (bounded sample)."""
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    cores = max(1, min(cores, 16))
+    ref = os.path.join(ROOT, "oracle", "_ref", "mpi_lsbsort")
+    mpirun = shutil.which("mpirun") or "/opt/conda/bin/mpirun"
+    if os.path.exists(ref) and os.path.exists(mpirun):
+        cmd = [mpirun, "-n", str(cores), ref, "--n", str(sample), "--no-verify"]
+        try:
+            out = subprocess.run(cmd, capture_output=True, text=True, timeout=240, check=True).stdout
+            m = re.search(r"That's ([0-9.eE+-]+) M elements sorted / s", out)
+            if m:
+                return {"value": float(m.group(1)), "unit": "Melem/s", "cores": cores,
+                        "kind": "reference",
+                        "sample": f"mpirun -n {cores} oracle/_ref/mpi_lsbsort --n {sample} --no-verify "
+                                  "(reference mpi/mpi_lsbsort.cpp, 16-bit digits, sort-only window)"}
+        except (subprocess.SubprocessError, OSError):
+            pass
+    # fallback: the oracle's single-threaded C restatement
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    n = min(sample, 1 << 24)
+    slots = oracle.generate_slots(n, 1)
+    t0 = time.perf_counter()
+    oracle.mpi_sort_slots(n, 1, slots, bits=16)
+    dt = time.perf_counter() - t0
+    return {"value": n / dt / 1e6, "unit": "Melem/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/lsb_oracle.c oracle_mpi_sort n={n} P=1 16-bit"}
+
+
+def main():
+    a = parse()
+    d = Dist()
+    N = d.world if d.world > 1 else a.gpus
+    if d.world > 1 and a.gpus != d.world:
+        N = d.world
+    n_total = a.n_per_gpu * N
+    if d.world > 1:
+        uid = lsbsort.get_unique_id() if d.rank == 0 else None
+        uid = d.bcast_bytes(uid)
+        w = lsbsort.World.rank(n_total, N, d.rank, d.local_rank, uid)
+    else:
+        if N != 1:
+            raise SystemExit("multi-GPU runs are launched one process per GPU (torch.distributed.run)")
+        w = lsbsort.World(n_total, ranks=1)
+
+    def step(timed):
+        w.generate()
+        w.barrier()
+        device_sync()
+        d.barrier()
+        t0 = time.perf_counter()
+        w.my_sort()
+        w.barrier()
+        device_sync()
+        d.barrier()
+        return time.perf_counter() - t0
+
+    for _ in range(a.warmup):
+        step(False)
+    w.reset_kernel_stats()
+    w.set_timing(True)
+    total = 0.0
+    for _ in range(a.steps):
+        total += step(True)
+    w.set_timing(False)
+    stats = w.kernel_stats()
+    scatter_elems = w.scatter_elems()
+    verified = None
+    if not a.no_verify:
+        ok, bad = w.verify()
+        verified = d.all_true(ok)
+    total = d.max(total)
+
+    ms_per_step = total / a.steps * 1e3
+    value = n_total * a.steps / total / 1e6
+    launches, scatter_ms = stats["scatter"]
+    workload = f"configs[1]: sort of 2^30 16-byte records per GPU, 8-bit digits, 8 passes, {N} GPU(s)"
+    roof = None
+    if launches and scatter_ms > 0:
+        elems_per_launch = scatter_elems / launches
+        avg_s = scatter_ms / launches / 1e3
+        achieved = SCATTER_BYTES_PER_ELEM * elems_per_launch / avg_s / 1e9
+        traffic = load_traffic(workload)
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "kernel": "k_scatter", "bytes_per_launch": int(SCATTER_BYTES_PER_ELEM * elems_per_launch),
+                "avg_launch_ms": round(scatter_ms / launches, 4)}
+    sort_gbs = PASS_BYTES_PER_ELEM * 8 * (n_total / N) / (ms_per_step / 1e3) / 1e9
+    out = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "Melem/s",
+        "n_gpus": N,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(value / REF_MPI_MELEMS, 3),
+        "dtype": "u64",
+        "data": "synthetic: pcg64(rank) keys, val = global index (mpi_lsbsort.cpp:650-656), regenerated on device before every step",
+        "config": {"workload": workload, "n_total": n_total, "n_per_gpu": a.n_per_gpu,
+                   "radix_bits": 8, "passes": 8, "record_bytes": 16,
+                   "parallelism": f"block partition over {N} GPU(s); per pass RCCL AllGather of counts + Send/Recv all-to-all" if N > 1 else "1 GPU, no exchange"},
+        "roofline": roof,
+        "sort_hbm_frac": round(sort_gbs / HBM_PEAK_GBS, 4),
+        "kernel_ms_per_step": {k: round(v[1] / a.steps, 3) for k, v in stats.items()},
+        "verified": verified,
+        "vs_baseline_basis": "MPI mpi_lsbsort 830 M elem/s (64 nodes x 128 cores, n=2^36; BASELINE.md §1)",
+    }
+    if d.rank == 0 and N == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(a.cpu_sample)
+    elif d.rank == 0:
+        out["cpu_baseline"] = None
+    w.close()
+    d.close()
+    if d.rank == 0:
+        print(json.dumps(out), flush=True)
+    if verified is False:
+        sys.exit(1)
+
+
+if __name__ == "__main__":
+    main()

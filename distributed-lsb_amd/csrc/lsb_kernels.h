@@ -1,0 +1,65 @@
+// Internal interface between the runtime (lsb_runtime.cpp) and the HIP
+// kernels (lsb_kernels.hip).  Not part of the C ABI (that is include/lsb.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace lsb {
+
+// == SortElement (mpi/mpi_lsbsort.cpp:29-32); lsb_elem_t in the ABI.
+struct alignas(16) Elem {
+  uint64_t key;
+  uint64_t val;
+};
+static_assert(sizeof(Elem) == 16, "16-byte records");
+
+constexpr int kDigitBits = 8;                 // one local pass = one 8-bit digit
+constexpr int kBuckets = 1 << kDigitBits;     // 256
+constexpr int kScatterBlock = 256;            // 4 waves
+constexpr int kScatterIpt = 16;               // items per thread
+constexpr int kTile = kScatterBlock * kScatterIpt;  // 4096 elements = 64 KiB in LDS
+constexpr int kMaxChunks = 1024;              // upper bound on the chunk grid
+
+// A rank's `m` elements are cut into `num_chunks` contiguous chunks of
+// `chunk_elems` (a multiple of kTile; the last may be short).  The count
+// (upsweep) and scatter kernels both run one workgroup per chunk, so the
+// per-chunk bucket counts of the former are the exact run offsets of the
+// latter.
+struct Chunking {
+  int64_t chunk_elems = 0;
+  int num_chunks = 0;
+};
+Chunking make_chunking(int64_t m, int max_chunks);
+
+// On-device PCG64 (pcg-cpp setseq_xsl_rr_128_64): A[i] = {pcg64(seed)[i], val0 + i}.
+hipError_t launch_pcg_fill(Elem* A, int64_t count, uint64_t seed, uint64_t val0, hipStream_t s);
+
+// chunk_hist[b * G + c] = number of elements of chunk c whose digit is b.
+hipError_t launch_upsweep(const Elem* A, int64_t m, int shift, Chunking ch,
+                          uint32_t* chunk_hist, hipStream_t s);
+
+// chunk_off[b * G + c] = sum_{c' < c} chunk_hist[b * G + c'];  totals[b] = row sum.
+hipError_t launch_scan(const uint32_t* chunk_hist, int G, uint64_t* chunk_off,
+                       uint64_t* totals, hipStream_t s);
+
+// Stable counting-sort scatter of one digit: out[pos] with
+// pos = bucket_start[b] + chunk_off[b][c] + rank of the element among the
+// chunk's digit-b elements (localShuffle, mpi/mpi_lsbsort.cpp:240-246).
+hipError_t launch_scatter(const Elem* in, Elem* out, int64_t m, int shift, Chunking ch,
+                          const uint64_t* chunk_off, const uint64_t* totals, hipStream_t s);
+
+// Receiver-side placement after the exchange: recv[k] (from source s, the
+// first s with k < rend[s]) goes to A[place_off[s * 256 + digit] + k].
+hipError_t launch_place(const Elem* recv, Elem* A, int64_t m, int shift, int P,
+                        const int64_t* rend, const int64_t* place_off, hipStream_t s);
+
+// O(n) bit-exact stable-sort check of a rank's here-part (see lsb_verify).
+// first_bad must hold UINT64_MAX before the launch; receives min bad global index.
+hipError_t launch_verify(const Elem* A, int64_t here, int64_t gbase, int64_t n, int64_t per,
+                         unsigned long long* first_bad, hipStream_t s);
+
+// Key-only local sortedness (checkSorted); *unsorted set to 1 on a descent.
+hipError_t launch_check_sorted(const Elem* A, int64_t here, unsigned int* unsorted, hipStream_t s);
+
+}  // namespace lsb

@@ -1,0 +1,457 @@
+// HIP kernels of the MI355X-native LSD radix sort (gfx950 / CDNA4).
+//
+// One local pass on one 8-bit digit, per rank, is reduce-then-scan:
+//   k_upsweep  per-chunk digit histogram         (count loop, mpi/mpi_lsbsort.cpp:226-229)
+//   k_scan     chunk x bucket exclusive scan      (starts, :232-238 / exclusiveScan :385-414)
+//   k_scatter  stable scatter through LDS         (shuffle loop, :241-246)
+// and, when P > 1, after the RCCL exchange,
+//   k_place    received runs -> final local slots (placement loop, :568-575)
+//
+// Everything is integer indexing, so the bound is HBM, not MFMA.  Design
+// points for CDNA4:
+//   * 16-byte records move as one dwordx4 per lane; tiles are read with
+//     consecutive lanes on consecutive records (1 KiB per wave-instruction).
+//   * Stable in-tile ranking uses 64-lane __ballot match masks (8 ballots
+//     for 8 bits): rank = popc(match & lanemask_lt) + a per-wave LDS counter,
+//     so equal digits never contend on an LDS atomic.
+//   * The ranked tile is staged in LDS (64 KiB) and written back in
+//     tile-sorted order, so each bucket's run leaves the CU as contiguous
+//     16-byte stores from consecutive lanes.
+#include "lsb_kernels.h"
+
+namespace lsb {
+namespace {
+
+typedef unsigned __int128 u128;
+
+constexpr u128 kPcgMult = ((u128)0x2360ED051FC65DA4ULL << 64) | (u128)0x4385DF649FCCF645ULL;
+constexpr u128 kPcgInc = ((u128)0x5851F42D4C957F2DULL << 64) | (u128)0x14057B7EF767814FULL;
+
+// LCG jump table: stepping 2^k times is s -> mul[k]*s + add[k].
+struct JumpTable {
+  uint64_t mul_lo[64], mul_hi[64], add_lo[64], add_hi[64];
+};
+
+constexpr JumpTable make_jump_table() {
+  JumpTable t{};
+  u128 m = kPcgMult, a = kPcgInc;
+  for (int k = 0; k < 64; ++k) {
+    t.mul_lo[k] = (uint64_t)m;
+    t.mul_hi[k] = (uint64_t)(m >> 64);
+    t.add_lo[k] = (uint64_t)a;
+    t.add_hi[k] = (uint64_t)(a >> 64);
+    a = a * (m + 1);
+    m = m * m;
+  }
+  return t;
+}
+
+__constant__ JumpTable kJump = make_jump_table();
+
+__device__ __forceinline__ uint64_t pcg_output(u128 s) {
+  const uint64_t x = (uint64_t)(s >> 64) ^ (uint64_t)s;
+  const unsigned rot = (unsigned)(s >> 122);
+  return (x >> rot) | (x << ((64u - rot) & 63u));
+}
+
+__device__ __forceinline__ u128 pcg_seed(uint64_t seed) {
+  return ((u128)seed + kPcgInc) * kPcgMult + kPcgInc;
+}
+
+// Advance by `delta` steps; the 2^k maps commute, so bit order is free.
+__device__ __forceinline__ u128 pcg_jump(u128 s, uint64_t delta) {
+  while (delta) {
+    const int k = __builtin_ctzll(delta);
+    const u128 m = ((u128)kJump.mul_hi[k] << 64) | kJump.mul_lo[k];
+    const u128 a = ((u128)kJump.add_hi[k] << 64) | kJump.add_lo[k];
+    s = s * m + a;
+    delta &= delta - 1;
+  }
+  return s;
+}
+
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+// popc(mask & lanemask_lt) in two instructions.
+__device__ __forceinline__ uint32_t mbcnt(uint64_t mask) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                   __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+// Lanes of `active` whose 8-bit digit equals mine.
+__device__ __forceinline__ uint64_t match_digit8(uint32_t d, uint64_t active) {
+  uint64_t m = active;
+#pragma unroll
+  for (int bit = 0; bit < 8; ++bit) {
+    const bool set = (d >> bit) & 1u;
+    const uint64_t bal = __ballot(set);
+    m &= set ? bal : ~bal;
+  }
+  return m;
+}
+
+__device__ __forceinline__ Elem load_elem(const Elem* p) {
+  const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(p);
+  return Elem{v.x, v.y};
+}
+
+__device__ __forceinline__ void store_elem(Elem* p, const Elem& e) {
+  *reinterpret_cast<ulonglong2*>(p) = make_ulonglong2(e.key, e.val);
+}
+
+// Inclusive wave scan (64 lanes).
+template <typename T>
+__device__ __forceinline__ T wave_inclusive_scan(T v) {
+  const uint32_t lane = lane_id();
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const T u = __shfl_up(v, off, 64);
+    if (lane >= (uint32_t)off) v += u;
+  }
+  return v;
+}
+
+// Exclusive scan over the whole workgroup (every thread must call it).
+// `tmp` needs BLOCK/64 entries.  *total receives the block sum.
+template <int BLOCK, typename T>
+__device__ __forceinline__ T block_exclusive_scan(T v, T* tmp, T* total) {
+  constexpr int W = BLOCK / 64;
+  const int w = threadIdx.x >> 6;
+  const T inc = wave_inclusive_scan(v);
+  if (lane_id() == 63) tmp[w] = inc;
+  __syncthreads();
+  T pre = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < W; ++i) {
+    const T x = tmp[i];
+    pre += (i < w) ? x : T(0);
+    tot += x;
+  }
+  __syncthreads();
+  *total = tot;
+  return pre + inc - v;
+}
+
+// ---------------------------------------------------------------- PCG fill
+constexpr int kFillPerThread = 16;
+
+__global__ __launch_bounds__(256) void k_pcg_fill(Elem* __restrict__ A, int64_t count,
+                                                  uint64_t seed, uint64_t val0) {
+  const int64_t first = ((int64_t)blockIdx.x * 256 + threadIdx.x) * kFillPerThread;
+  if (first >= count) return;
+  u128 s = pcg_jump(pcg_seed(seed), (uint64_t)first);
+  const int64_t last = first + kFillPerThread < count ? first + kFillPerThread : count;
+  for (int64_t i = first; i < last; ++i) {
+    s = s * kPcgMult + kPcgInc;  // operator(): bump, then output the new state
+    store_elem(A + i, Elem{pcg_output(s), val0 + (uint64_t)i});
+  }
+}
+
+// ----------------------------------------------------------------- upsweep
+template <int BLOCK, int IPT>
+__global__ __launch_bounds__(BLOCK) void k_upsweep(const Elem* __restrict__ A, int64_t m,
+                                                   int shift, int64_t chunk_elems, int G,
+                                                   uint32_t* __restrict__ chunk_hist) {
+  __shared__ uint32_t hist[kBuckets];
+  for (int b = threadIdx.x; b < kBuckets; b += BLOCK) hist[b] = 0;
+  __syncthreads();
+
+  const int c = blockIdx.x;
+  const int64_t beg = (int64_t)c * chunk_elems;
+  const int64_t end = beg + chunk_elems < m ? beg + chunk_elems : m;
+  const uint64_t* __restrict__ keys = reinterpret_cast<const uint64_t*>(A);
+
+  for (int64_t tb = beg; tb < end; tb += (int64_t)BLOCK * IPT) {
+    uint64_t k[IPT];
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+      const int64_t idx = tb + (int64_t)i * BLOCK + threadIdx.x;
+      k[i] = idx < end ? keys[2 * idx] : 0ull;
+    }
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+      const int64_t idx = tb + (int64_t)i * BLOCK + threadIdx.x;
+      const bool valid = idx < end;
+      const uint32_t d = (uint32_t)(k[i] >> shift) & (kBuckets - 1);
+      const uint64_t mt = match_digit8(d, __ballot(valid));
+      if (valid && mbcnt(mt) == 0) atomicAdd(&hist[d], (uint32_t)__popcll(mt));
+    }
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < kBuckets; b += BLOCK) chunk_hist[(int64_t)b * G + c] = hist[b];
+}
+
+// -------------------------------------------------------------------- scan
+constexpr int kScanBlock = 256;
+constexpr int kScanPer = kMaxChunks / kScanBlock;  // 4
+
+__global__ __launch_bounds__(kScanBlock) void k_scan(const uint32_t* __restrict__ chunk_hist,
+                                                     int G, uint64_t* __restrict__ chunk_off,
+                                                     uint64_t* __restrict__ totals) {
+  __shared__ uint64_t tmp[kScanBlock / 64];
+  const int b = blockIdx.x;
+  const uint32_t* row = chunk_hist + (int64_t)b * G;
+  uint32_t v[kScanPer];
+  uint64_t sum = 0;
+#pragma unroll
+  for (int j = 0; j < kScanPer; ++j) {
+    const int c = threadIdx.x * kScanPer + j;
+    v[j] = c < G ? row[c] : 0u;
+    sum += v[j];
+  }
+  uint64_t total;
+  uint64_t pre = block_exclusive_scan<kScanBlock>(sum, tmp, &total);
+#pragma unroll
+  for (int j = 0; j < kScanPer; ++j) {
+    const int c = threadIdx.x * kScanPer + j;
+    if (c < G) chunk_off[(int64_t)b * G + c] = pre;
+    pre += v[j];
+  }
+  if (threadIdx.x == 0) totals[b] = total;
+}
+
+// ----------------------------------------------------------------- scatter
+// One workgroup walks its chunk tile by tile.  A tile is split wave-major:
+// wave w owns tile elements [w*64*IPT, (w+1)*64*IPT) and its item i is the
+// 64 consecutive elements starting at w*64*IPT + i*64, so tile order is
+// (wave, item, lane) and every load is a coalesced 1 KiB wave-instruction.
+template <int BLOCK, int IPT>
+__global__ __launch_bounds__(BLOCK, 2) void k_scatter(const Elem* __restrict__ in,
+                                                      Elem* __restrict__ out, int64_t m,
+                                                      int shift, int64_t chunk_elems, int G,
+                                                      const uint64_t* __restrict__ chunk_off,
+                                                      const uint64_t* __restrict__ totals) {
+  constexpr int W = BLOCK / 64;
+  constexpr int T = BLOCK * IPT;
+  static_assert(BLOCK >= kBuckets, "one thread per bucket in the offset phase");
+
+  __shared__ Elem stage[T];                 // the ranked tile (64 KiB)
+  __shared__ uint32_t wcnt[W][kBuckets];    // per-wave digit counters -> positions
+  __shared__ int64_t delta[kBuckets];       // global dest = delta[digit] + tile position
+  __shared__ uint64_t scan64[W];
+  __shared__ uint32_t scan32[W];
+
+  const int t = threadIdx.x;
+  const int w = t >> 6;
+  const uint32_t lane = lane_id();
+  const int c = blockIdx.x;
+  const int64_t beg = (int64_t)c * chunk_elems;
+  const int64_t end = beg + chunk_elems < m ? beg + chunk_elems : m;
+
+  // Global start of this chunk's run of each bucket.
+  uint64_t run = 0;
+  {
+    const uint64_t tot = t < kBuckets ? totals[t] : 0ull;
+    uint64_t all;
+    const uint64_t bstart = block_exclusive_scan<BLOCK>(tot, scan64, &all);
+    if (t < kBuckets) run = bstart + chunk_off[(int64_t)t * G + c];
+  }
+
+  for (int64_t tb = beg; tb < end; tb += T) {
+    const int nvalid = (int)((end - tb) < T ? (end - tb) : T);
+
+#pragma unroll
+    for (int j = 0; j < kBuckets / 64; ++j) wcnt[w][lane + 64 * j] = 0;
+
+    Elem e[IPT];
+    const int wbase = w * 64 * IPT + (int)lane;
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+      const int li = wbase + i * 64;
+      e[i] = li < nvalid ? load_elem(in + tb + li) : Elem{0ull, 0ull};
+    }
+
+    // Stable rank of every element among the wave's elements of its digit.
+    uint32_t rk[IPT];
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+      const bool valid = wbase + i * 64 < nvalid;
+      const uint32_t d = (uint32_t)(e[i].key >> shift) & (kBuckets - 1);
+      const uint64_t mt = match_digit8(d, __ballot(valid));
+      const uint32_t below = mbcnt(mt);
+      const uint32_t pre = wcnt[w][d];
+      rk[i] = pre + below;
+      if (valid && below == 0) wcnt[w][d] = pre + (uint32_t)__popcll(mt);
+    }
+    __syncthreads();
+
+    // Per digit: wave-exclusive prefix, tile-local start, global delta.
+    uint32_t cnt = 0;
+    if (t < kBuckets) {
+#pragma unroll
+      for (int ww = 0; ww < W; ++ww) {
+        const uint32_t x = wcnt[ww][t];
+        wcnt[ww][t] = cnt;
+        cnt += x;
+      }
+    }
+    uint32_t tile_total;
+    const uint32_t lstart = block_exclusive_scan<BLOCK>(cnt, scan32, &tile_total);
+    if (t < kBuckets) {
+#pragma unroll
+      for (int ww = 0; ww < W; ++ww) wcnt[ww][t] += lstart;
+      delta[t] = (int64_t)run - (int64_t)lstart;
+      run += cnt;
+    }
+    __syncthreads();
+
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+      if (wbase + i * 64 < nvalid) {
+        const uint32_t d = (uint32_t)(e[i].key >> shift) & (kBuckets - 1);
+        stage[wcnt[w][d] + rk[i]] = e[i];
+      }
+    }
+    __syncthreads();
+
+    for (int j = t; j < nvalid; j += BLOCK) {
+      const Elem x = stage[j];
+      const uint32_t d = (uint32_t)(x.key >> shift) & (kBuckets - 1);
+      store_elem(out + (delta[d] + j), x);
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------- place
+constexpr int kPlaceBlock = 256;
+constexpr int kPlaceLdsRanks = 16;  // P * 256 offsets (32 KiB) staged in LDS up to here
+
+template <bool kLds>
+__global__ __launch_bounds__(kPlaceBlock) void k_place(const Elem* __restrict__ recv,
+                                                       Elem* __restrict__ A, int64_t m, int shift,
+                                                       int P, const int64_t* __restrict__ rend,
+                                                       const int64_t* __restrict__ place_off) {
+  __shared__ int64_t lds_off[kLds ? kPlaceLdsRanks * kBuckets : 1];
+  __shared__ int64_t lds_end[kLds ? kPlaceLdsRanks : 1];
+  const int64_t* off = place_off;
+  const int64_t* ends = rend;
+  if (kLds) {
+    for (int i = threadIdx.x; i < P * kBuckets; i += kPlaceBlock) lds_off[i] = place_off[i];
+    for (int i = threadIdx.x; i < P; i += kPlaceBlock) lds_end[i] = rend[i];
+    __syncthreads();
+    off = lds_off;
+    ends = lds_end;
+  }
+  const int64_t stride = (int64_t)gridDim.x * kPlaceBlock;
+  for (int64_t k = (int64_t)blockIdx.x * kPlaceBlock + threadIdx.x; k < m; k += stride) {
+    const Elem x = load_elem(recv + k);
+    int s = 0;
+    while (s < P - 1 && k >= ends[s]) ++s;  // first source whose segment holds k
+    const uint32_t d = (uint32_t)(x.key >> shift) & (kBuckets - 1);
+    store_elem(A + (off[s * kBuckets + d] + k), x);
+  }
+}
+
+// ------------------------------------------------------------------ checks
+__global__ __launch_bounds__(256) void k_verify(const Elem* __restrict__ A, int64_t here,
+                                                int64_t gbase, int64_t n, int64_t per,
+                                                unsigned long long* first_bad) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < here; i += stride) {
+    const Elem x = load_elem(A + i);
+    bool bad = x.val >= (uint64_t)n;
+    if (!bad) {
+      const uint64_t r = x.val / (uint64_t)per;
+      const uint64_t idx = x.val - r * (uint64_t)per;
+      bad = pcg_output(pcg_jump(pcg_seed(r), idx + 1)) != x.key;
+    }
+    if (i + 1 < here) {
+      const Elem y = load_elem(A + i + 1);
+      bad |= !(x.key < y.key || (x.key == y.key && x.val < y.val));
+    }
+    if (bad) atomicMin(first_bad, (unsigned long long)(gbase + i));
+  }
+}
+
+__global__ __launch_bounds__(256) void k_check_sorted(const Elem* __restrict__ A, int64_t here,
+                                                      unsigned int* unsorted) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i + 1 < here; i += stride) {
+    if (A[i + 1].key < A[i].key) *unsorted = 1u;
+  }
+}
+
+int grid_for(int64_t work, int block, int cap) {
+  const int64_t g = (work + block - 1) / block;
+  return (int)(g < 1 ? 1 : (g > cap ? cap : g));
+}
+
+}  // namespace
+
+Chunking make_chunking(int64_t m, int max_chunks) {
+  Chunking ch;
+  if (m <= 0) return ch;
+  if (max_chunks > kMaxChunks) max_chunks = kMaxChunks;
+  if (max_chunks < 1) max_chunks = 1;
+  const int64_t tiles = (m + kTile - 1) / kTile;
+  const int64_t tiles_per_chunk = (tiles + max_chunks - 1) / max_chunks;
+  ch.chunk_elems = tiles_per_chunk * kTile;
+  ch.num_chunks = (int)((m + ch.chunk_elems - 1) / ch.chunk_elems);
+  return ch;
+}
+
+hipError_t launch_pcg_fill(Elem* A, int64_t count, uint64_t seed, uint64_t val0, hipStream_t s) {
+  if (count <= 0) return hipSuccess;
+  const int64_t threads = (count + kFillPerThread - 1) / kFillPerThread;
+  const int64_t blocks = (threads + 255) / 256;
+  hipLaunchKernelGGL(k_pcg_fill, dim3((unsigned)blocks), dim3(256), 0, s, A, count, seed, val0);
+  return hipGetLastError();
+}
+
+hipError_t launch_upsweep(const Elem* A, int64_t m, int shift, Chunking ch, uint32_t* chunk_hist,
+                          hipStream_t s) {
+  if (m <= 0) return hipSuccess;
+  hipLaunchKernelGGL((k_upsweep<256, 16>), dim3(ch.num_chunks), dim3(256), 0, s, A, m, shift,
+                     ch.chunk_elems, ch.num_chunks, chunk_hist);
+  return hipGetLastError();
+}
+
+hipError_t launch_scan(const uint32_t* chunk_hist, int G, uint64_t* chunk_off, uint64_t* totals,
+                       hipStream_t s) {
+  if (G <= 0) return hipSuccess;
+  if (G > kMaxChunks) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_scan, dim3(kBuckets), dim3(kScanBlock), 0, s, chunk_hist, G, chunk_off,
+                     totals);
+  return hipGetLastError();
+}
+
+hipError_t launch_scatter(const Elem* in, Elem* out, int64_t m, int shift, Chunking ch,
+                          const uint64_t* chunk_off, const uint64_t* totals, hipStream_t s) {
+  if (m <= 0) return hipSuccess;
+  hipLaunchKernelGGL((k_scatter<kScatterBlock, kScatterIpt>), dim3(ch.num_chunks),
+                     dim3(kScatterBlock), 0, s, in, out, m, shift, ch.chunk_elems, ch.num_chunks,
+                     chunk_off, totals);
+  return hipGetLastError();
+}
+
+hipError_t launch_place(const Elem* recv, Elem* A, int64_t m, int shift, int P, const int64_t* rend,
+                        const int64_t* place_off, hipStream_t s) {
+  if (m <= 0) return hipSuccess;
+  if (P < 1) return hipErrorInvalidValue;
+  const dim3 grid(grid_for(m, kPlaceBlock, 4096));
+  if (P <= kPlaceLdsRanks)
+    hipLaunchKernelGGL(k_place<true>, grid, dim3(kPlaceBlock), 0, s, recv, A, m, shift, P, rend,
+                       place_off);
+  else
+    hipLaunchKernelGGL(k_place<false>, grid, dim3(kPlaceBlock), 0, s, recv, A, m, shift, P, rend,
+                       place_off);
+  return hipGetLastError();
+}
+
+hipError_t launch_verify(const Elem* A, int64_t here, int64_t gbase, int64_t n, int64_t per,
+                         unsigned long long* first_bad, hipStream_t s) {
+  if (here <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_verify, dim3(grid_for(here, 256, 8192)), dim3(256), 0, s, A, here, gbase, n,
+                     per, first_bad);
+  return hipGetLastError();
+}
+
+hipError_t launch_check_sorted(const Elem* A, int64_t here, unsigned int* unsorted, hipStream_t s) {
+  if (here <= 1) return hipSuccess;
+  hipLaunchKernelGGL(k_check_sorted, dim3(grid_for(here, 256, 8192)), dim3(256), 0, s, A, here,
+                     unsorted);
+  return hipGetLastError();
+}
+
+}  // namespace lsb

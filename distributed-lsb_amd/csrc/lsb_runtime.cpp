@@ -1,0 +1,821 @@
+// Runtime behind include/lsb.h: contexts, device buffers, the pass loop
+// (mySort / globalShuffle) and the exchange (RCCL or in-process loopback).
+//
+// Per pass on digit d (64 / 8 passes, least significant first,
+// mpi/mpi_lsbsort.cpp:580-585), for every rank r:
+//   1. local stable pass A -> B on digit d            k_upsweep, k_scan, k_scatter
+//      (localShuffle, mpi/mpi_lsbsort.cpp:213-247).  B is then bucket-ordered.
+//   P == 1: B is the answer for this digit; A and B swap.
+//   P  > 1:
+//   2. all-gather of the 256 bucket counts of every rank
+//      (replaces copyCountsToGlobalCounts + MPI_Exscan + copyStartsFromGlobalStarts,
+//       mpi/mpi_lsbsort.cpp:327-479: every rank then scans the P x 256 matrix
+//       in digit-major, rank-minor order itself)
+//   3. host plan: per-peer send/recv counts and the placement table
+//   4. all-to-all-v of the 16-byte records (MPI_Alltoallv of 24-byte
+//      ShuffleBufSortElement at mpi/mpi_lsbsort.cpp:563; here no dst index
+//      travels: the receiver derives it from the gathered counts)
+//   5. k_place: received runs -> A (mpi/mpi_lsbsort.cpp:568-575)
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/lsb.h"
+#include "lsb_kernels.h"
+
+using lsb::Elem;
+
+namespace {
+
+enum class Mode { kLoopback, kRccl };
+
+struct PendingEvent {
+  int kid;
+  int dev;
+  hipEvent_t start, stop;
+};
+
+struct Rank {
+  int rank = 0;
+  int dev = 0;
+  hipStream_t stream = nullptr;
+  int64_t here = 0;
+  Elem* A = nullptr;  // per slots: input / output (DistributedArray A)
+  Elem* B = nullptr;  // per slots: scratch; the bucket-ordered send buffer when P > 1
+  Elem* R = nullptr;  // per slots: receive buffer (P > 1 only)
+  uint32_t* chunk_hist = nullptr;       // [256][kMaxChunks]
+  uint64_t* chunk_off = nullptr;        // [256][kMaxChunks]
+  uint64_t* totals = nullptr;           // [256]  local bucket counts of the current digit
+  uint64_t* gather = nullptr;           // [P][256] all-gathered counts (RCCL mode)
+  int64_t* place = nullptr;             // [P][256] place_off, then [P] rend
+  unsigned long long* check = nullptr;  // [4] verify / check_sorted scratch
+  uint64_t* gather_h = nullptr;         // pinned host mirrors
+  int64_t* place_h = nullptr;
+  lsb::Chunking chunking;
+  int max_chunks = 0;
+  std::vector<int64_t> send_counts, send_displs, recv_counts, recv_displs;
+};
+
+}  // namespace
+
+struct lsb_ctx {
+  Mode mode = Mode::kLoopback;
+  int64_t n = 0;
+  int64_t per = 0;
+  int P = 1;
+  int bits = 8;
+  int first_rank = 0;
+  std::vector<Rank> ranks;  // local ranks
+  ncclComm_t comm = nullptr;
+  bool timing = false;
+  bool force_exchange = false;
+  std::vector<PendingEvent> pending;
+  std::vector<hipEvent_t> event_pool;
+  int64_t launches[LSB_K_COUNT] = {};
+  double total_ms[LSB_K_COUNT] = {};
+  int64_t scatter_elems = 0;
+  std::vector<int64_t> hist_h;  // [P][256] as int64 for the planner
+};
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char* what, const char* detail) {
+  char buf[512];
+  snprintf(buf, sizeof buf, "%s: %s", what, detail ? detail : "");
+  g_last_error = buf;
+  if (getenv("LSB_DEBUG")) fprintf(stderr, "[lsb] %s\n", buf);
+  return code;
+}
+
+#define HIP_TRY(expr)                                                    \
+  do {                                                                   \
+    hipError_t _e = (expr);                                              \
+    if (_e != hipSuccess) return fail(LSB_ERR_HIP, #expr, hipGetErrorString(_e)); \
+  } while (0)
+
+#define RCCL_TRY(expr)                                                   \
+  do {                                                                   \
+    ncclResult_t _r = (expr);                                            \
+    if (_r != ncclSuccess) return fail(LSB_ERR_RCCL, #expr, ncclGetErrorString(_r)); \
+  } while (0)
+
+#define LSB_TRY(expr)              \
+  do {                             \
+    int _c = (expr);               \
+    if (_c != LSB_OK) return _c;   \
+  } while (0)
+
+int64_t div_ceil(int64_t x, int64_t y) { return (x + y - 1) / y; }
+
+int64_t here_of(int64_t n, int P, int r) {
+  const int64_t per = P > 0 ? div_ceil(n, P) : 0;
+  int64_t h = per;
+  if (per * r + h > n) h = n - per * r;
+  return h < 0 ? 0 : h;
+}
+
+bool exchanging(const lsb_ctx* c) { return c->P > 1 || c->force_exchange; }
+
+// ---- timing -------------------------------------------------------------
+hipEvent_t take_event(lsb_ctx* c) {
+  if (!c->event_pool.empty()) {
+    hipEvent_t e = c->event_pool.back();
+    c->event_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+struct Timer {
+  lsb_ctx* c;
+  Rank* r;
+  int kid;
+  hipEvent_t start = nullptr;
+  Timer(lsb_ctx* c_, Rank* r_, int kid_) : c(c_), r(r_), kid(kid_) {
+    if (!c->timing) return;
+    start = take_event(c);
+    if (start) (void)hipEventRecord(start, r->stream);
+  }
+  void stop() {
+    if (!start) return;
+    hipEvent_t e = take_event(c);
+    if (!e) return;
+    (void)hipEventRecord(e, r->stream);
+    c->pending.push_back({kid, r->dev, start, e});
+    start = nullptr;
+  }
+  ~Timer() { stop(); }
+};
+
+int resolve_timing(lsb_ctx* c) {
+  for (auto& p : c->pending) {
+    HIP_TRY(hipSetDevice(p.dev));
+    HIP_TRY(hipEventSynchronize(p.stop));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, p.start, p.stop));
+    c->launches[p.kid] += 1;
+    c->total_ms[p.kid] += ms;
+    c->event_pool.push_back(p.start);
+    c->event_pool.push_back(p.stop);
+  }
+  c->pending.clear();
+  return LSB_OK;
+}
+
+// ---- allocation -----------------------------------------------------------
+template <typename T>
+int dev_alloc(T** p, size_t count) {
+  *p = nullptr;
+  if (count == 0) count = 1;
+  hipError_t e = hipMalloc(reinterpret_cast<void**>(p), count * sizeof(T));
+  if (e != hipSuccess) return fail(LSB_ERR_NOMEM, "hipMalloc", hipGetErrorString(e));
+  return LSB_OK;
+}
+
+template <typename T>
+int host_alloc(T** p, size_t count) {
+  *p = nullptr;
+  if (count == 0) count = 1;
+  hipError_t e = hipHostMalloc(reinterpret_cast<void**>(p), count * sizeof(T), 0);
+  if (e != hipSuccess) return fail(LSB_ERR_NOMEM, "hipHostMalloc", hipGetErrorString(e));
+  return LSB_OK;
+}
+
+int max_chunks_for_device(int dev) {
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) != hipSuccess || prop.multiProcessorCount <= 0) return 512;
+  // Two scatter workgroups fit one CU (70 KiB LDS each): one chunk per slot.
+  return std::min(lsb::kMaxChunks, 2 * prop.multiProcessorCount);
+}
+
+int init_rank(lsb_ctx* c, Rank& r, int rank, int dev) {
+  r.rank = rank;
+  r.dev = dev;
+  r.here = here_of(c->n, c->P, rank);
+  HIP_TRY(hipSetDevice(dev));
+  HIP_TRY(hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking));
+  const size_t per = (size_t)c->per;
+  LSB_TRY(dev_alloc(&r.A, per));
+  LSB_TRY(dev_alloc(&r.B, per));
+  if (exchanging(c) || c->P > 1) LSB_TRY(dev_alloc(&r.R, per));
+  const size_t hist_entries = (size_t)lsb::kBuckets * lsb::kMaxChunks;
+  LSB_TRY(dev_alloc(&r.chunk_hist, hist_entries));
+  LSB_TRY(dev_alloc(&r.chunk_off, hist_entries));
+  LSB_TRY(dev_alloc(&r.totals, lsb::kBuckets));
+  LSB_TRY(dev_alloc(&r.gather, (size_t)c->P * lsb::kBuckets));
+  LSB_TRY(dev_alloc(&r.place, (size_t)c->P * lsb::kBuckets + c->P));
+  LSB_TRY(dev_alloc(&r.check, 4));
+  LSB_TRY(host_alloc(&r.gather_h, (size_t)c->P * lsb::kBuckets));
+  LSB_TRY(host_alloc(&r.place_h, (size_t)c->P * lsb::kBuckets + c->P));
+  r.max_chunks = max_chunks_for_device(dev);
+  r.chunking = lsb::make_chunking(r.here, r.max_chunks);
+  r.send_counts.assign(c->P, 0);
+  r.send_displs.assign(c->P, 0);
+  r.recv_counts.assign(c->P, 0);
+  r.recv_displs.assign(c->P, 0);
+  return LSB_OK;
+}
+
+void free_rank(Rank& r) {
+  if (r.stream) {
+    (void)hipSetDevice(r.dev);
+    (void)hipStreamSynchronize(r.stream);
+  }
+  (void)hipFree(r.A);
+  (void)hipFree(r.B);
+  (void)hipFree(r.R);
+  (void)hipFree(r.chunk_hist);
+  (void)hipFree(r.chunk_off);
+  (void)hipFree(r.totals);
+  (void)hipFree(r.gather);
+  (void)hipFree(r.place);
+  (void)hipFree(r.check);
+  (void)hipHostFree(r.gather_h);
+  (void)hipHostFree(r.place_h);
+  if (r.stream) (void)hipStreamDestroy(r.stream);
+  r = Rank();
+}
+
+Rank* local_rank(lsb_ctx* c, int rank) {
+  const int i = rank - c->first_rank;
+  if (i < 0 || i >= (int)c->ranks.size()) return nullptr;
+  return &c->ranks[i];
+}
+
+// ---- one local stable pass A -> B (localShuffle) ------------------------
+int local_pass(lsb_ctx* c, Rank& r, int shift) {
+  if (r.here == 0) {
+    HIP_TRY(hipSetDevice(r.dev));
+    HIP_TRY(hipMemsetAsync(r.totals, 0, sizeof(uint64_t) * lsb::kBuckets, r.stream));
+    return LSB_OK;
+  }
+  HIP_TRY(hipSetDevice(r.dev));
+  const lsb::Chunking& ch = r.chunking;
+  {
+    Timer t(c, &r, LSB_K_UPSWEEP);
+    HIP_TRY(lsb::launch_upsweep(r.A, r.here, shift, ch, r.chunk_hist, r.stream));
+  }
+  {
+    Timer t(c, &r, LSB_K_SCAN);
+    HIP_TRY(lsb::launch_scan(r.chunk_hist, ch.num_chunks, r.chunk_off, r.totals, r.stream));
+  }
+  {
+    Timer t(c, &r, LSB_K_SCATTER);
+    HIP_TRY(lsb::launch_scatter(r.A, r.B, r.here, shift, ch, r.chunk_off, r.totals, r.stream));
+    if (c->timing) c->scatter_elems += r.here;
+  }
+  return LSB_OK;
+}
+
+// Turn the host plan of rank r into the device placement table.
+int upload_plan(lsb_ctx* c, Rank& r) {
+  const int P = c->P;
+  int64_t* rend = r.place_h + (size_t)P * lsb::kBuckets;
+  int64_t acc = 0;
+  for (int s = 0; s < P; ++s) {
+    acc += r.recv_counts[s];
+    rend[s] = acc;
+  }
+  HIP_TRY(hipSetDevice(r.dev));
+  HIP_TRY(hipMemcpyAsync(r.place, r.place_h, sizeof(int64_t) * ((size_t)P * lsb::kBuckets + P),
+                         hipMemcpyHostToDevice, r.stream));
+  return LSB_OK;
+}
+
+int plan_rank(lsb_ctx* c, Rank& r) {
+  return lsb_plan_exchange(c->n, c->P, r.rank, lsb::kBuckets, c->hist_h.data(), r.send_counts.data(),
+                           r.send_displs.data(), r.recv_counts.data(), r.recv_displs.data(),
+                           r.place_h);
+}
+
+int place_rank(lsb_ctx* c, Rank& r, int shift) {
+  Timer t(c, &r, LSB_K_PLACE);
+  HIP_TRY(hipSetDevice(r.dev));
+  const int64_t* rend = r.place + (size_t)c->P * lsb::kBuckets;
+  HIP_TRY(lsb::launch_place(r.R, r.A, r.here, shift, c->P, rend, r.place, r.stream));
+  return LSB_OK;
+}
+
+// ---- exchange: in-process loopback --------------------------------------
+int exchange_loopback(lsb_ctx* c, int shift) {
+  // counts of every rank -> host (stands in for ncclAllGather)
+  for (Rank& r : c->ranks) {
+    HIP_TRY(hipSetDevice(r.dev));
+    HIP_TRY(hipMemcpyAsync(r.gather_h, r.totals, sizeof(uint64_t) * lsb::kBuckets,
+                           hipMemcpyDeviceToHost, r.stream));
+  }
+  for (Rank& r : c->ranks) {
+    HIP_TRY(hipSetDevice(r.dev));
+    HIP_TRY(hipStreamSynchronize(r.stream));
+  }
+  for (Rank& r : c->ranks)
+    for (int b = 0; b < lsb::kBuckets; ++b)
+      c->hist_h[(size_t)r.rank * lsb::kBuckets + b] = (int64_t)r.gather_h[b];
+  for (Rank& r : c->ranks) {
+    LSB_TRY(plan_rank(c, r));
+    LSB_TRY(upload_plan(c, r));
+  }
+  // all-to-all-v: segment q of rank s's bucket-ordered B -> rank q's R.
+  for (Rank& q : c->ranks) {
+    Timer t(c, &q, LSB_K_EXCHANGE);
+    HIP_TRY(hipSetDevice(q.dev));
+    for (Rank& s : c->ranks) {
+      const int64_t cnt = s.send_counts[q.rank];
+      if (cnt != q.recv_counts[s.rank])
+        return fail(LSB_ERR_STATE, "exchange_loopback", "send/recv count mismatch");
+      if (cnt == 0) continue;
+      HIP_TRY(hipMemcpyAsync(q.R + q.recv_displs[s.rank], s.B + s.send_displs[q.rank],
+                             (size_t)cnt * sizeof(Elem), hipMemcpyDefault, q.stream));
+    }
+  }
+  for (Rank& r : c->ranks) LSB_TRY(place_rank(c, r, shift));
+  // The next pass rewrites every B that these copies read, on other streams.
+  for (Rank& r : c->ranks) {
+    HIP_TRY(hipSetDevice(r.dev));
+    HIP_TRY(hipStreamSynchronize(r.stream));
+  }
+  return LSB_OK;
+}
+
+// ---- exchange: RCCL (one rank per process) ------------------------------
+int exchange_rccl(lsb_ctx* c, int shift) {
+  const int P = c->P;
+  Rank& r = c->ranks[0];
+  HIP_TRY(hipSetDevice(r.dev));
+  {
+    Timer t(c, &r, LSB_K_EXCHANGE);
+    RCCL_TRY(ncclAllGather(r.totals, r.gather, lsb::kBuckets, ncclUint64, c->comm, r.stream));
+  }
+  HIP_TRY(hipMemcpyAsync(r.gather_h, r.gather, sizeof(uint64_t) * (size_t)P * lsb::kBuckets,
+                         hipMemcpyDeviceToHost, r.stream));
+  HIP_TRY(hipStreamSynchronize(r.stream));
+  for (size_t i = 0; i < (size_t)P * lsb::kBuckets; ++i) c->hist_h[i] = (int64_t)r.gather_h[i];
+  LSB_TRY(plan_rank(c, r));
+  LSB_TRY(upload_plan(c, r));
+  {
+    Timer t(c, &r, LSB_K_EXCHANGE);
+    const int me = r.rank;
+    // The self segment is a device copy; the P-1 peers go over RCCL.
+    if (r.send_counts[me] != r.recv_counts[me])
+      return fail(LSB_ERR_STATE, "exchange_rccl", "self count mismatch");
+    if (r.send_counts[me] > 0)
+      HIP_TRY(hipMemcpyAsync(r.R + r.recv_displs[me], r.B + r.send_displs[me],
+                             (size_t)r.send_counts[me] * sizeof(Elem), hipMemcpyDeviceToDevice,
+                             r.stream));
+    RCCL_TRY(ncclGroupStart());
+    for (int q = 0; q < P; ++q) {
+      if (q == me) continue;
+      if (r.send_counts[q] > 0)
+        RCCL_TRY(ncclSend(r.B + r.send_displs[q], (size_t)r.send_counts[q] * 2, ncclUint64, q,
+                          c->comm, r.stream));
+      if (r.recv_counts[q] > 0)
+        RCCL_TRY(ncclRecv(r.R + r.recv_displs[q], (size_t)r.recv_counts[q] * 2, ncclUint64, q,
+                          c->comm, r.stream));
+    }
+    RCCL_TRY(ncclGroupEnd());
+  }
+  return place_rank(c, r, shift);
+}
+
+int do_pass(lsb_ctx* c, int digit) {
+  const int shift = digit * lsb::kDigitBits;
+  for (Rank& r : c->ranks) LSB_TRY(local_pass(c, r, shift));
+  if (!exchanging(c)) {
+    for (Rank& r : c->ranks) std::swap(r.A, r.B);
+    return LSB_OK;
+  }
+  if (c->mode == Mode::kRccl) return exchange_rccl(c, shift);
+  return exchange_loopback(c, shift);
+}
+
+int check_ctx(const lsb_ctx* c) {
+  if (!c) return fail(LSB_ERR_INVALID, "lsb", "null context");
+  return LSB_OK;
+}
+
+int finish_create(lsb_ctx* c, lsb_ctx_t** out) {
+  *out = c;
+  return LSB_OK;
+}
+
+// Boundary records of every rank (first, last of its here-part), gathered on
+// the host: [rank][0..3] = first.key, first.val, last.key, last.val.
+int gather_boundaries(lsb_ctx* c, std::vector<uint64_t>& bnd) {
+  const int P = c->P;
+  bnd.assign((size_t)P * 4, 0);
+  if (c->mode == Mode::kLoopback) {
+    for (Rank& r : c->ranks) {
+      if (r.here == 0) continue;
+      HIP_TRY(hipSetDevice(r.dev));
+      HIP_TRY(hipMemcpy(&bnd[(size_t)r.rank * 4], r.A, 16, hipMemcpyDeviceToHost));
+      HIP_TRY(hipMemcpy(&bnd[(size_t)r.rank * 4 + 2], r.A + (r.here - 1), 16, hipMemcpyDeviceToHost));
+    }
+    return LSB_OK;
+  }
+  Rank& r = c->ranks[0];
+  HIP_TRY(hipSetDevice(r.dev));
+  uint64_t* d = r.gather;  // reuse: needs 4*P <= 256*P entries
+  HIP_TRY(hipMemsetAsync(d, 0, sizeof(uint64_t) * 4 * P, r.stream));
+  if (r.here > 0) {
+    HIP_TRY(hipMemcpyAsync(d + (size_t)r.rank * 4, r.A, 16, hipMemcpyDeviceToDevice, r.stream));
+    HIP_TRY(hipMemcpyAsync(d + (size_t)r.rank * 4 + 2, r.A + (r.here - 1), 16,
+                           hipMemcpyDeviceToDevice, r.stream));
+  }
+  // Each rank contributes its own 4 words (in place all-gather).
+  RCCL_TRY(ncclAllGather(d + (size_t)r.rank * 4, d, 4, ncclUint64, c->comm, r.stream));
+  HIP_TRY(hipMemcpyAsync(bnd.data(), d, sizeof(uint64_t) * 4 * P, hipMemcpyDeviceToHost, r.stream));
+  HIP_TRY(hipStreamSynchronize(r.stream));
+  return LSB_OK;
+}
+
+int allreduce_min_i64(lsb_ctx* c, int64_t* v) {
+  if (c->mode == Mode::kLoopback) return LSB_OK;
+  Rank& r = c->ranks[0];
+  HIP_TRY(hipSetDevice(r.dev));
+  int64_t* d = reinterpret_cast<int64_t*>(r.check);
+  HIP_TRY(hipMemcpyAsync(d, v, sizeof(int64_t), hipMemcpyHostToDevice, r.stream));
+  RCCL_TRY(ncclAllReduce(d, d, 1, ncclInt64, ncclMin, c->comm, r.stream));
+  HIP_TRY(hipMemcpyAsync(v, d, sizeof(int64_t), hipMemcpyDeviceToHost, r.stream));
+  HIP_TRY(hipStreamSynchronize(r.stream));
+  return LSB_OK;
+}
+
+}  // namespace
+
+// ======================================================================
+extern "C" {
+
+int64_t lsb_per_rank(int64_t n_total, int num_ranks) {
+  return (num_ranks > 0 && n_total >= 0) ? div_ceil(n_total, num_ranks) : 0;
+}
+
+int64_t lsb_here(int64_t n_total, int num_ranks, int rank) {
+  if (num_ranks <= 0 || n_total < 0 || rank < 0 || rank >= num_ranks) return 0;
+  return here_of(n_total, num_ranks, rank);
+}
+
+const char* lsb_strerror(int code) {
+  switch (code) {
+    case LSB_OK: return "ok";
+    case LSB_ERR_INVALID: return "invalid argument";
+    case LSB_ERR_HIP: return g_last_error.empty() ? "HIP error" : g_last_error.c_str();
+    case LSB_ERR_RCCL: return g_last_error.empty() ? "RCCL error" : g_last_error.c_str();
+    case LSB_ERR_NOMEM: return "out of memory";
+    case LSB_ERR_VERIFY: return "verification failed";
+    case LSB_ERR_UNSUPPORTED: return "unsupported";
+    case LSB_ERR_STATE: return g_last_error.empty() ? "invalid state" : g_last_error.c_str();
+    default: return "unknown error";
+  }
+}
+
+int lsb_create(lsb_ctx_t** out, int64_t n_total, int num_ranks, const int* dev_ids,
+               int radix_bits) {
+  if (!out) return fail(LSB_ERR_INVALID, "lsb_create", "null out");
+  *out = nullptr;
+  if (n_total < 0 || num_ranks < 1) return fail(LSB_ERR_INVALID, "lsb_create", "n or P");
+  if (radix_bits != 8) return fail(LSB_ERR_UNSUPPORTED, "lsb_create", "radix_bits must be 8");
+  lsb_ctx* c = new (std::nothrow) lsb_ctx();
+  if (!c) return LSB_ERR_NOMEM;
+  c->mode = Mode::kLoopback;
+  c->n = n_total;
+  c->P = num_ranks;
+  c->per = div_ceil(n_total, num_ranks);
+  c->bits = radix_bits;
+  c->first_rank = 0;
+  c->hist_h.assign((size_t)num_ranks * lsb::kBuckets, 0);
+  c->ranks.resize(num_ranks);
+  for (int r = 0; r < num_ranks; ++r) {
+    int rc = init_rank(c, c->ranks[r], r, dev_ids ? dev_ids[r] : 0);
+    if (rc != LSB_OK) {
+      lsb_destroy(c);
+      return rc;
+    }
+  }
+  return finish_create(c, out);
+}
+
+int lsb_get_unique_id(unsigned char id[LSB_UNIQUE_ID_BYTES]) {
+  if (!id) return fail(LSB_ERR_INVALID, "lsb_get_unique_id", "null");
+  ncclUniqueId uid;
+  RCCL_TRY(ncclGetUniqueId(&uid));
+  static_assert(sizeof(uid) == LSB_UNIQUE_ID_BYTES, "id size");
+  memcpy(id, &uid, sizeof uid);
+  return LSB_OK;
+}
+
+int lsb_create_rank(lsb_ctx_t** out, int64_t n_total, int num_ranks, int rank, int dev_id,
+                    int radix_bits, const unsigned char id[LSB_UNIQUE_ID_BYTES]) {
+  if (!out) return fail(LSB_ERR_INVALID, "lsb_create_rank", "null out");
+  *out = nullptr;
+  if (n_total < 0 || num_ranks < 1 || rank < 0 || rank >= num_ranks || !id)
+    return fail(LSB_ERR_INVALID, "lsb_create_rank", "n, P, rank or id");
+  if (radix_bits != 8) return fail(LSB_ERR_UNSUPPORTED, "lsb_create_rank", "radix_bits must be 8");
+  lsb_ctx* c = new (std::nothrow) lsb_ctx();
+  if (!c) return LSB_ERR_NOMEM;
+  c->mode = Mode::kRccl;
+  c->n = n_total;
+  c->P = num_ranks;
+  c->per = div_ceil(n_total, num_ranks);
+  c->bits = radix_bits;
+  c->first_rank = rank;
+  c->hist_h.assign((size_t)num_ranks * lsb::kBuckets, 0);
+  c->ranks.resize(1);
+  int rc = init_rank(c, c->ranks[0], rank, dev_id);
+  if (rc == LSB_OK) {
+    ncclUniqueId uid;
+    memcpy(&uid, id, sizeof uid);
+    if (hipSetDevice(dev_id) != hipSuccess) rc = fail(LSB_ERR_HIP, "hipSetDevice", "");
+    else {
+      ncclResult_t nr = ncclCommInitRank(&c->comm, num_ranks, uid, rank);
+      if (nr != ncclSuccess) {
+        c->comm = nullptr;
+        rc = fail(LSB_ERR_RCCL, "ncclCommInitRank", ncclGetErrorString(nr));
+      }
+    }
+  }
+  if (rc != LSB_OK) {
+    lsb_destroy(c);
+    return rc;
+  }
+  return finish_create(c, out);
+}
+
+void lsb_destroy(lsb_ctx_t* c) {
+  if (!c) return;
+  (void)resolve_timing(c);
+  for (Rank& r : c->ranks) free_rank(r);
+  for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
+  if (c->comm) (void)ncclCommDestroy(c->comm);
+  delete c;
+}
+
+int lsb_set_option(lsb_ctx_t* c, int option, int64_t value) {
+  LSB_TRY(check_ctx(c));
+  switch (option) {
+    case LSB_OPT_TIMING:
+      c->timing = value != 0;
+      return LSB_OK;
+    case LSB_OPT_FORCE_EXCHANGE:
+      if (value && c->P == 1) {
+        for (Rank& r : c->ranks)
+          if (!r.R) {
+            HIP_TRY(hipSetDevice(r.dev));
+            LSB_TRY(dev_alloc(&r.R, (size_t)c->per));
+          }
+      }
+      c->force_exchange = value != 0;
+      return LSB_OK;
+    default:
+      return fail(LSB_ERR_INVALID, "lsb_set_option", "unknown option");
+  }
+}
+
+int lsb_local_ranks(const lsb_ctx_t* c, int* first_rank, int* num_local) {
+  LSB_TRY(check_ctx(c));
+  if (first_rank) *first_rank = c->first_rank;
+  if (num_local) *num_local = (int)c->ranks.size();
+  return LSB_OK;
+}
+
+int lsb_generate(lsb_ctx_t* c) {
+  LSB_TRY(check_ctx(c));
+  for (Rank& r : c->ranks) {
+    HIP_TRY(hipSetDevice(r.dev));
+    // Every one of the `per` slots, like mpi/mpi_lsbsort.cpp:650-656.
+    HIP_TRY(lsb::launch_pcg_fill(r.A, c->per, (uint64_t)r.rank, (uint64_t)r.rank * c->per,
+                                 r.stream));
+  }
+  return lsb_sync(c);
+}
+
+int lsb_copy_in(lsb_ctx_t* c, int rank, int64_t off, int64_t cnt, const lsb_elem_t* host) {
+  LSB_TRY(check_ctx(c));
+  Rank* r = local_rank(c, rank);
+  if (!r || off < 0 || cnt < 0 || off + cnt > c->per || (cnt > 0 && !host))
+    return fail(LSB_ERR_INVALID, "lsb_copy_in", "rank or range");
+  if (cnt == 0) return LSB_OK;
+  HIP_TRY(hipSetDevice(r->dev));
+  HIP_TRY(hipStreamSynchronize(r->stream));
+  HIP_TRY(hipMemcpy(r->A + off, host, (size_t)cnt * sizeof(Elem), hipMemcpyHostToDevice));
+  return LSB_OK;
+}
+
+int lsb_copy_out(lsb_ctx_t* c, int rank, int64_t off, int64_t cnt, lsb_elem_t* host) {
+  LSB_TRY(check_ctx(c));
+  Rank* r = local_rank(c, rank);
+  if (!r || off < 0 || cnt < 0 || off + cnt > c->per || (cnt > 0 && !host))
+    return fail(LSB_ERR_INVALID, "lsb_copy_out", "rank or range");
+  if (cnt == 0) return LSB_OK;
+  HIP_TRY(hipSetDevice(r->dev));
+  HIP_TRY(hipStreamSynchronize(r->stream));
+  HIP_TRY(hipMemcpy(host, r->A + off, (size_t)cnt * sizeof(Elem), hipMemcpyDeviceToHost));
+  return LSB_OK;
+}
+
+int lsb_pass(lsb_ctx_t* c, int digit) {
+  LSB_TRY(check_ctx(c));
+  if (digit < 0 || digit >= 64 / c->bits) return fail(LSB_ERR_INVALID, "lsb_pass", "digit");
+  return do_pass(c, digit);
+}
+
+int lsb_sort(lsb_ctx_t* c) {
+  LSB_TRY(check_ctx(c));
+  std::vector<Timer> sort_timers;
+  sort_timers.reserve(c->ranks.size());
+  for (Rank& r : c->ranks) sort_timers.emplace_back(c, &r, LSB_K_SORT);
+  const int passes = 64 / c->bits;
+  for (int d = 0; d < passes; ++d) LSB_TRY(do_pass(c, d));
+  for (Timer& t : sort_timers) t.stop();
+  return LSB_OK;
+}
+
+int lsb_sync(lsb_ctx_t* c) {
+  LSB_TRY(check_ctx(c));
+  for (Rank& r : c->ranks) {
+    HIP_TRY(hipSetDevice(r.dev));
+    HIP_TRY(hipStreamSynchronize(r.stream));
+  }
+  return LSB_OK;
+}
+
+int lsb_barrier(lsb_ctx_t* c) {
+  LSB_TRY(lsb_sync(c));
+  if (c->mode != Mode::kRccl) return LSB_OK;
+  Rank& r = c->ranks[0];
+  HIP_TRY(hipSetDevice(r.dev));
+  RCCL_TRY(ncclAllReduce(r.check, r.check, 1, ncclUint64, ncclSum, c->comm, r.stream));
+  HIP_TRY(hipStreamSynchronize(r.stream));
+  return LSB_OK;
+}
+
+int lsb_verify(lsb_ctx_t* c, int64_t* first_bad) {
+  LSB_TRY(check_ctx(c));
+  int64_t bad = INT64_MAX;
+  for (Rank& r : c->ranks) {
+    HIP_TRY(hipSetDevice(r.dev));
+    HIP_TRY(hipMemsetAsync(r.check, 0xff, sizeof(unsigned long long), r.stream));
+    HIP_TRY(lsb::launch_verify(r.A, r.here, (int64_t)r.rank * c->per, c->n, c->per, r.check,
+                               r.stream));
+    unsigned long long h = ~0ull;
+    HIP_TRY(hipMemcpyAsync(&h, r.check, sizeof h, hipMemcpyDeviceToHost, r.stream));
+    HIP_TRY(hipStreamSynchronize(r.stream));
+    if (h != ~0ull && (int64_t)h < bad) bad = (int64_t)h;
+  }
+  // Rank boundaries: last record of each non-empty rank < first of the next.
+  std::vector<uint64_t> bnd;
+  LSB_TRY(gather_boundaries(c, bnd));
+  int prev = -1;
+  for (int s = 0; s < c->P; ++s) {
+    if (here_of(c->n, c->P, s) == 0) continue;
+    if (prev >= 0) {
+      const uint64_t lk = bnd[(size_t)prev * 4 + 2], lv = bnd[(size_t)prev * 4 + 3];
+      const uint64_t fk = bnd[(size_t)s * 4 + 0], fv = bnd[(size_t)s * 4 + 1];
+      if (!(lk < fk || (lk == fk && lv < fv))) {
+        const int64_t idx = (int64_t)prev * c->per + here_of(c->n, c->P, prev) - 1;
+        if (idx < bad) bad = idx;
+      }
+    }
+    prev = s;
+  }
+  LSB_TRY(allreduce_min_i64(c, &bad));
+  if (first_bad) *first_bad = bad == INT64_MAX ? -1 : bad;
+  return bad == INT64_MAX ? LSB_OK : LSB_ERR_VERIFY;
+}
+
+int lsb_check_sorted(lsb_ctx_t* c, int* sorted) {
+  LSB_TRY(check_ctx(c));
+  int64_t bad = 0;  // 0 = sorted so far; reduced with min over "sorted" flags
+  int local_ok = 1;
+  for (Rank& r : c->ranks) {
+    HIP_TRY(hipSetDevice(r.dev));
+    HIP_TRY(hipMemsetAsync(r.check, 0, sizeof(unsigned int), r.stream));
+    HIP_TRY(lsb::launch_check_sorted(r.A, r.here, reinterpret_cast<unsigned int*>(r.check),
+                                     r.stream));
+    unsigned int h = 0;
+    HIP_TRY(hipMemcpyAsync(&h, r.check, sizeof h, hipMemcpyDeviceToHost, r.stream));
+    HIP_TRY(hipStreamSynchronize(r.stream));
+    if (h) local_ok = 0;
+  }
+  std::vector<uint64_t> bnd;
+  LSB_TRY(gather_boundaries(c, bnd));
+  int prev = -1;
+  int bounds_ok = 1;
+  for (int s = 0; s < c->P; ++s) {
+    if (here_of(c->n, c->P, s) == 0) continue;
+    if (prev >= 0 && bnd[(size_t)s * 4 + 0] < bnd[(size_t)prev * 4 + 2]) bounds_ok = 0;
+    prev = s;
+  }
+  bad = (local_ok && bounds_ok) ? 1 : 0;
+  LSB_TRY(allreduce_min_i64(c, &bad));
+  if (sorted) *sorted = (int)bad;
+  return LSB_OK;
+}
+
+int lsb_get_kernel_stats(lsb_ctx_t* c, int kid, int64_t* launches, double* total_ms) {
+  LSB_TRY(check_ctx(c));
+  if (kid < 0 || kid >= LSB_K_COUNT) return fail(LSB_ERR_INVALID, "lsb_get_kernel_stats", "id");
+  LSB_TRY(resolve_timing(c));
+  if (launches) *launches = c->launches[kid];
+  if (total_ms) *total_ms = c->total_ms[kid];
+  return LSB_OK;
+}
+
+int lsb_reset_kernel_stats(lsb_ctx_t* c) {
+  LSB_TRY(check_ctx(c));
+  LSB_TRY(resolve_timing(c));
+  for (int k = 0; k < LSB_K_COUNT; ++k) {
+    c->launches[k] = 0;
+    c->total_ms[k] = 0.0;
+  }
+  c->scatter_elems = 0;
+  return LSB_OK;
+}
+
+int lsb_get_scatter_elems(lsb_ctx_t* c, int64_t* elems) {
+  LSB_TRY(check_ctx(c));
+  if (elems) *elems = c->scatter_elems;
+  return LSB_OK;
+}
+
+// Host planner: see include/lsb.h.  For rank `me`, the global destination of
+// its j-th bucket-b record is gstart[b][me] + j with
+//   gstart[b][s] = sum_{b'<b} total[b'] + sum_{s'<s} hist[s'][b]
+// (GlobalCounts[digit*P + rank] scanned, mpi/mpi_lsbsort.cpp:350,378,401-412),
+// and owner(g) = g / per (globalIdxToLocalIdx, mpi/mpi_lsbsort.cpp:113-120).
+int lsb_plan_exchange(int64_t n_total, int P, int me, int nb, const int64_t* hist,
+                      int64_t* send_counts, int64_t* send_displs, int64_t* recv_counts,
+                      int64_t* recv_displs, int64_t* place_off) {
+  if (P < 1 || me < 0 || me >= P || nb < 1 || n_total < 0 || !hist || !send_counts ||
+      !send_displs || !recv_counts || !recv_displs || !place_off)
+    return fail(LSB_ERR_INVALID, "lsb_plan_exchange", "arguments");
+  const int64_t per = div_ceil(n_total, P);
+  for (int q = 0; q < P; ++q) send_counts[q] = recv_counts[q] = 0;
+  const int64_t lo_me = (int64_t)me * per;
+  const int64_t hi_me = lo_me + here_of(n_total, P, me);
+  // Two sweeps over buckets in global order; base = start of bucket b.
+  int64_t base = 0;
+  // Receive side is built in (s, b) order but the stream from s is ordered
+  // by b, so first collect per-source run pieces, then lay them out.
+  std::vector<int64_t> piece_lo((size_t)P * nb, 0), piece_len((size_t)P * nb, 0);
+  for (int b = 0; b < nb; ++b) {
+    int64_t acc = base;
+    int64_t total_b = 0;
+    for (int s = 0; s < P; ++s) {
+      const int64_t h = hist[(size_t)s * nb + b];
+      if (h < 0) return fail(LSB_ERR_INVALID, "lsb_plan_exchange", "negative count");
+      const int64_t g0 = acc, g1 = acc + h;
+      if (s == me && h > 0 && per > 0) {
+        // split my run [g0, g1) over the owners
+        int64_t g = g0;
+        while (g < g1) {
+          const int64_t q = g / per;
+          const int64_t qend = std::min(g1, (q + 1) * per);
+          if (q >= P) return fail(LSB_ERR_INVALID, "lsb_plan_exchange", "counts exceed n");
+          send_counts[q] += qend - g;
+          g = qend;
+        }
+      }
+      // part of source s's run that lands in my range
+      const int64_t lo = std::max(g0, lo_me), hi = std::min(g1, hi_me);
+      if (hi > lo) {
+        piece_lo[(size_t)s * nb + b] = lo;
+        piece_len[(size_t)s * nb + b] = hi - lo;
+        recv_counts[s] += hi - lo;
+      }
+      acc = g1;
+      total_b += h;
+    }
+    base += total_b;
+  }
+  if (base > n_total) return fail(LSB_ERR_INVALID, "lsb_plan_exchange", "counts exceed n");
+  int64_t acc = 0;
+  for (int q = 0; q < P; ++q) {
+    send_displs[q] = acc;
+    acc += send_counts[q];
+  }
+  acc = 0;
+  for (int s = 0; s < P; ++s) {
+    recv_displs[s] = acc;
+    int64_t k = acc;  // recv index where source s's next piece starts
+    for (int b = 0; b < nb; ++b) {
+      const size_t i = (size_t)s * nb + b;
+      place_off[i] = (piece_lo[i] - lo_me) - k;
+      k += piece_len[i];
+    }
+    acc += recv_counts[s];
+  }
+  return LSB_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,276 @@
+// hip_lsbsort — the MI355X peer of mpi/mpi_lsbsort.cpp and shmem/shmem_lsbsort.cpp.
+//
+// Same command line (--n N, --print, --verify, --no-verify; verify defaults
+// to on iff n < 128Mi, mpi/mpi_lsbsort.cpp:591-611), same input (pcg64(rank),
+// val = global index), same timing window (sort only, between barriers,
+// :688-699) and the same output lines; the sort itself runs on GPUs through
+// the C ABI in include/lsb.h.
+//
+// Ranks:
+//   --gpus P   one process per GPU (rank r on device r), exchange over RCCL;
+//              this program forks the P rank processes itself, before any HIP
+//              call, the way mpirun would start them.
+//   --ranks P  P logical ranks driven by this one process on --device D
+//              (default 0), exchange by device copies; same results as
+//              `mpirun -n P mpi_lsbsort` on one GPU.
+//   --json     also print one machine-readable line.
+#include <sys/wait.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cinttypes>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "lsb.h"
+
+namespace {
+
+struct Options {
+  int64_t n = 100LL * 1000 * 1000;
+  bool print = false;
+  bool verify = false;
+  bool verify_set = false;
+  int gpus = 0;
+  int ranks = 1;
+  int device = 0;
+  bool json = false;
+};
+
+void flush_output() {
+  // mpi/mpi_lsbsort.cpp:163-169 flushes and sleeps so rank output interleaves
+  // in order; here ranks are ordered by barriers, a flush is enough.
+  fflush(stdout);
+}
+
+void die(const char* what, int rc) {
+  fprintf(stderr, "hip_lsbsort: %s failed: %s\n", what, lsb_strerror(rc));
+  fflush(stderr);
+  _exit(2);
+}
+
+#define CHECK(call)                 \
+  do {                              \
+    int _rc = (call);               \
+    if (_rc != LSB_OK) die(#call, _rc); \
+  } while (0)
+
+struct World {
+  lsb_ctx_t* ctx = nullptr;
+  int P = 1;
+  int first = 0;
+  int nlocal = 1;
+  int64_t n = 0;
+  int64_t per = 0;
+  bool root() const { return first == 0; }
+  bool is_local(int r) const { return r >= first && r < first + nlocal; }
+};
+
+// DistributedArray::print (mpi/mpi_lsbsort.cpp:171-200).
+void print_array(World& w, const char* name, int64_t n_per_rank) {
+  CHECK(lsb_barrier(w.ctx));
+  if (w.root()) {
+    if (n_per_rank * w.P >= w.n)
+      printf("%s: displaying all %" PRId64 " elements\n", name, w.n);
+    else
+      printf("%s: displaying first %" PRId64 " elements on each rank out of %" PRId64
+             " elements\n", name, n_per_rank, w.n);
+  }
+  std::vector<lsb_elem_t> buf(n_per_rank);
+  for (int r = 0; r < w.P; ++r) {
+    if (w.is_local(r)) {
+      const int64_t here = lsb_here(w.n, w.P, r);
+      const int64_t k = here < n_per_rank ? here : n_per_rank;
+      CHECK(lsb_copy_out(w.ctx, r, 0, k, buf.data()));
+      for (int64_t i = 0; i < k; ++i)
+        printf("%s[%" PRId64 "] = (%016" PRIx64 ",%" PRIu64 ")\n", name, r * w.per + i,
+               buf[i].key, buf[i].val);
+      if (k < here) printf("...\n");
+      flush_output();
+    }
+    CHECK(lsb_barrier(w.ctx));
+  }
+}
+
+int run(World& w, const Options& o) {
+  if (w.root()) {
+    printf("Total number of HIP ranks: %d\n", w.P);
+    printf("Problem size: %" PRId64 "\n", o.n);
+    flush_output();
+  }
+  {
+    auto start = std::chrono::steady_clock::now();
+    if (w.root()) {
+      printf("Generating random values\n");
+      flush_output();
+    }
+    CHECK(lsb_generate(w.ctx));
+    CHECK(lsb_barrier(w.ctx));
+    auto end = std::chrono::steady_clock::now();
+    if (w.root()) {
+      printf("Generated random values in %g s\n", std::chrono::duration<double>(end - start).count());
+      flush_output();
+    }
+    CHECK(lsb_barrier(w.ctx));
+  }
+  if (o.print) print_array(w, "A", 10);
+
+  double elapsed = 0;
+  {
+    if (w.root()) {
+      printf("Sorting\n");
+      flush_output();
+    }
+    CHECK(lsb_barrier(w.ctx));
+    auto start = std::chrono::steady_clock::now();
+    CHECK(lsb_sort(w.ctx));
+    CHECK(lsb_barrier(w.ctx));
+    auto end = std::chrono::steady_clock::now();
+    elapsed = std::chrono::duration<double>(end - start).count();
+    if (w.root()) {
+      printf("Sorted %" PRId64 " values in %g\n", o.n, elapsed);
+      printf("That's %g M elements sorted / s\n", o.n / elapsed / 1000.0 / 1000.0);
+      flush_output();
+    }
+    CHECK(lsb_barrier(w.ctx));
+  }
+  if (o.print) print_array(w, "A", 10);
+
+  int status = 0;
+  if (o.verify) {
+    if (w.root()) {
+      printf("Verifying\n");
+      flush_output();
+    }
+    int64_t first_bad = -1;
+    const int rc = lsb_verify(w.ctx, &first_bad);
+    if (rc == LSB_ERR_VERIFY) {
+      if (w.root()) printf("Sorted element %" PRId64 " did not match\n", first_bad);
+      status = 1;
+    } else if (rc != LSB_OK) {
+      die("lsb_verify", rc);
+    }
+    int sorted = 0;
+    CHECK(lsb_check_sorted(w.ctx, &sorted));
+    if (w.root()) printf(sorted ? "Array is sorted\n" : "Array is NOT sorted\n");
+    if (!sorted) status = 1;
+    flush_output();
+  }
+  if (o.json && w.root()) {
+    printf("{\"n\": %" PRId64 ", \"ranks\": %d, \"sort_s\": %.9g, \"melem_per_s\": %.6g, "
+           "\"verified\": %s}\n", o.n, w.P, elapsed, o.n / elapsed / 1e6,
+           o.verify ? (status == 0 ? "true" : "false") : "null");
+    flush_output();
+  }
+  return status;
+}
+
+int run_rank_process(const Options& o, int rank, int read_fd, const std::vector<int>& write_fds) {
+  unsigned char id[LSB_UNIQUE_ID_BYTES];
+  if (rank == 0) {
+    CHECK(lsb_get_unique_id(id));
+    for (int fd : write_fds)
+      if (write(fd, id, sizeof id) != (ssize_t)sizeof id) die("write unique id", LSB_ERR_STATE);
+  } else {
+    size_t got = 0;
+    while (got < sizeof id) {
+      ssize_t k = read(read_fd, id + got, sizeof id - got);
+      if (k <= 0) die("read unique id", LSB_ERR_STATE);
+      got += (size_t)k;
+    }
+  }
+  World w;
+  w.P = o.gpus;
+  w.n = o.n;
+  w.per = lsb_per_rank(o.n, o.gpus);
+  w.first = rank;
+  w.nlocal = 1;
+  CHECK(lsb_create_rank(&w.ctx, o.n, o.gpus, rank, rank, 8, id));
+  const int status = run(w, o);
+  lsb_destroy(w.ctx);
+  return status;
+}
+
+}  // namespace
+
+int main(int argc, char* argv[]) {
+  Options o;
+  for (int i = 1; i < argc; i++) {
+    const std::string a = argv[i];
+    auto next = [&](void) -> const char* {
+      if (i + 1 >= argc) {
+        fprintf(stderr, "missing value for %s\n", a.c_str());
+        exit(2);
+      }
+      return argv[++i];
+    };
+    if (a == "--n") o.n = std::stoll(next());
+    else if (a == "--print") o.print = true;
+    else if (a == "--verify") { o.verify = true; o.verify_set = true; }
+    else if (a == "--no-verify") { o.verify = false; o.verify_set = true; }
+    else if (a == "--gpus") o.gpus = std::stoi(next());
+    else if (a == "--ranks") o.ranks = std::stoi(next());
+    else if (a == "--device") o.device = std::stoi(next());
+    else if (a == "--json") o.json = true;
+  }
+  if (!o.verify_set) o.verify = (o.n < 128LL * 1024 * 1024);
+  if (o.n < 0 || o.ranks < 1 || o.gpus < 0) {
+    fprintf(stderr, "invalid arguments\n");
+    return 2;
+  }
+
+  if (o.gpus >= 1) {
+    // One process per GPU.  Fork every rank before anything touches HIP;
+    // rank 0 sends the RCCL unique id to the others through pipes.
+    std::vector<int> rd(o.gpus, -1), wr(o.gpus, -1);
+    for (int r = 1; r < o.gpus; ++r) {
+      int fds[2];
+      if (pipe(fds) != 0) {
+        perror("pipe");
+        return 2;
+      }
+      rd[r] = fds[0];
+      wr[r] = fds[1];
+    }
+    std::vector<pid_t> kids;
+    for (int r = 0; r < o.gpus; ++r) {
+      pid_t pid = fork();
+      if (pid < 0) {
+        perror("fork");
+        return 2;
+      }
+      if (pid == 0) {
+        std::vector<int> mine;
+        if (r == 0)
+          for (int q = 1; q < o.gpus; ++q) mine.push_back(wr[q]);
+        const int st = run_rank_process(o, r, rd[r], mine);
+        fflush(stdout);
+        _exit(st);
+      }
+      kids.push_back(pid);
+    }
+    int worst = 0;
+    for (pid_t pid : kids) {
+      int st = 0;
+      if (waitpid(pid, &st, 0) < 0) worst = 2;
+      else if (WIFEXITED(st)) worst = WEXITSTATUS(st) > worst ? WEXITSTATUS(st) : worst;
+      else worst = 2;
+    }
+    return worst;
+  }
+
+  World w;
+  w.P = o.ranks;
+  w.n = o.n;
+  w.per = lsb_per_rank(o.n, o.ranks);
+  w.first = 0;
+  w.nlocal = o.ranks;
+  std::vector<int> devs(o.ranks, o.device);
+  CHECK(lsb_create(&w.ctx, o.n, o.ranks, devs.data(), 8));
+  const int status = run(w, o);
+  lsb_destroy(w.ctx);
+  return status;
+}

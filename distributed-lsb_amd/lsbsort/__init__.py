@@ -1,0 +1,310 @@
+"""Python front end of the MI355X-native distributed LSD radix sort.
+
+A thin ctypes binding of the C ABI in ``include/lsb.h`` (library
+``distributed-lsb_amd/build/liblsb.so``), mirroring the reference's own
+seams so tests read like the reference program:
+
+  ==========================  ==============================================
+  reference                   here
+  ==========================  ==============================================
+  DistributedArray::create    ``World(n, ranks)`` / ``World.rank(...)``
+  (mpi/mpi_lsbsort.cpp:137)   (block partition per = ceil(n/P))
+  PCG init (:643-666)         ``World.generate()``
+  mySort(A, B) (:580-585)     ``World.my_sort()``   (alias ``mySort``)
+  globalShuffle (:481-577)    ``World.global_shuffle(d)`` (alias ``globalShuffle``)
+  verify (:710-738)           ``World.verify()``
+  checkSorted (shmem :180)    ``World.check_sorted()``
+  A.print(10) (:171-200)      ``World.print_lines("A", 10)``
+  ==========================  ==============================================
+
+Errors from the library raise :class:`LsbError` (the reference aborts on
+MPI errors, mpi/mpi_lsbsort.cpp:17-19).  There is no CPU fallback: if the
+HIP library is missing or no GPU is present, calls fail loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional, Sequence
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+ROOT_DIR = os.path.dirname(PKG_DIR)
+LIB_PATH = os.path.join(ROOT_DIR, "build", "liblsb.so")
+HARNESS_PATH = os.path.join(ROOT_DIR, "build", "hip_lsbsort")
+HEADER_PATH = os.path.join(os.path.dirname(ROOT_DIR), "include", "lsb.h")
+
+ELEM_DTYPE = np.dtype([("key", "<u8"), ("val", "<u8")])
+UNIQUE_ID_BYTES = 128
+
+LSB_OK = 0
+LSB_ERR_VERIFY = 5
+K_UPSWEEP, K_SCAN, K_SCATTER, K_EXCHANGE, K_PLACE, K_SORT = range(6)
+KERNEL_NAMES = ("upsweep", "scan", "scatter", "exchange", "place", "sort")
+OPT_TIMING, OPT_FORCE_EXCHANGE = 0, 1
+
+
+class LsbError(RuntimeError):
+    def __init__(self, code: int, where: str):
+        msg = _lib().lsb_strerror(code).decode()
+        super().__init__(f"{where}: lsb error {code}: {msg}")
+        self.code = code
+
+
+_L = None
+
+
+def _lib() -> ctypes.CDLL:
+    global _L
+    if _L is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"HIP library {LIB_PATH} is not built; run `make -C distributed-lsb_amd` "
+                "(or __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        i64, i32, vp, cp = ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_char_p
+        P64 = ctypes.POINTER(ctypes.c_int64)
+        sig = {
+            "lsb_per_rank": (i64, [i64, i32]),
+            "lsb_here": (i64, [i64, i32, i32]),
+            "lsb_create": (i32, [ctypes.POINTER(vp), i64, i32, ctypes.POINTER(ctypes.c_int), i32]),
+            "lsb_get_unique_id": (i32, [ctypes.c_char_p]),
+            "lsb_create_rank": (i32, [ctypes.POINTER(vp), i64, i32, i32, i32, i32, ctypes.c_char_p]),
+            "lsb_destroy": (None, [vp]),
+            "lsb_set_option": (i32, [vp, i32, i64]),
+            "lsb_local_ranks": (i32, [vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+            "lsb_generate": (i32, [vp]),
+            "lsb_copy_in": (i32, [vp, i32, i64, i64, vp]),
+            "lsb_copy_out": (i32, [vp, i32, i64, i64, vp]),
+            "lsb_sort": (i32, [vp]),
+            "lsb_pass": (i32, [vp, i32]),
+            "lsb_sync": (i32, [vp]),
+            "lsb_barrier": (i32, [vp]),
+            "lsb_verify": (i32, [vp, P64]),
+            "lsb_check_sorted": (i32, [vp, ctypes.POINTER(ctypes.c_int)]),
+            "lsb_get_kernel_stats": (i32, [vp, i32, P64, ctypes.POINTER(ctypes.c_double)]),
+            "lsb_reset_kernel_stats": (i32, [vp]),
+            "lsb_get_scatter_elems": (i32, [vp, P64]),
+            "lsb_plan_exchange": (i32, [i64, i32, i32, i32, vp, vp, vp, vp, vp, vp]),
+            "lsb_strerror": (cp, [i32]),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _L = L
+    return _L
+
+
+def _check(code: int, where: str) -> None:
+    if code != LSB_OK:
+        raise LsbError(code, where)
+
+
+def per_rank(n: int, P: int) -> int:
+    return int(_lib().lsb_per_rank(n, P))
+
+
+def here(n: int, P: int, r: int) -> int:
+    return int(_lib().lsb_here(n, P, r))
+
+
+def get_unique_id() -> bytes:
+    buf = ctypes.create_string_buffer(UNIQUE_ID_BYTES)
+    _check(_lib().lsb_get_unique_id(buf), "lsb_get_unique_id")
+    return buf.raw
+
+
+def plan_exchange(n: int, P: int, rank: int, hist: np.ndarray) -> dict:
+    """Host planner of rank `rank` for a P x nbuckets count matrix."""
+    hist = np.ascontiguousarray(hist, dtype=np.int64)
+    if hist.ndim != 2 or hist.shape[0] != P:
+        raise ValueError("hist must be P x nbuckets")
+    nb = hist.shape[1]
+    out = {k: np.zeros(P, dtype=np.int64) for k in
+           ("send_counts", "send_displs", "recv_counts", "recv_displs")}
+    out["place_off"] = np.zeros((P, nb), dtype=np.int64)
+    _check(_lib().lsb_plan_exchange(
+        n, P, rank, nb, hist.ctypes.data, out["send_counts"].ctypes.data,
+        out["send_displs"].ctypes.data, out["recv_counts"].ctypes.data,
+        out["recv_displs"].ctypes.data, out["place_off"].ctypes.data), "lsb_plan_exchange")
+    return out
+
+
+class World:
+    """One sort context: a block-distributed pair of arrays A, B over P ranks.
+
+    ``World(n, ranks=P)`` drives all P ranks from this process (logical
+    ranks; ``devices[r]`` per rank, default all on device 0).
+    ``World.rank(n, P, r, device, uid)`` is one rank of a multi-process RCCL
+    world (one process per GPU).
+    """
+
+    def __init__(self, n: int, ranks: int = 1, devices: Optional[Sequence[int]] = None,
+                 radix_bits: int = 8, _handle=None, _P=None):
+        self._h = ctypes.c_void_p()
+        if _handle is not None:
+            self._h = _handle
+            self.P = _P
+        else:
+            devs = None
+            if devices is not None:
+                if len(devices) != ranks:
+                    raise ValueError("one device per rank")
+                devs = (ctypes.c_int * ranks)(*devices)
+            _check(_lib().lsb_create(ctypes.byref(self._h), n, ranks, devs, radix_bits),
+                   "lsb_create")
+            self.P = ranks
+        self.n = n
+        self.per = per_rank(n, self.P)
+        self.radix_bits = radix_bits
+        first, nl = ctypes.c_int(), ctypes.c_int()
+        _check(_lib().lsb_local_ranks(self._h, ctypes.byref(first), ctypes.byref(nl)),
+               "lsb_local_ranks")
+        self.local_ranks = list(range(first.value, first.value + nl.value))
+
+    @classmethod
+    def rank(cls, n: int, num_ranks: int, rank: int, device: int, unique_id: bytes,
+             radix_bits: int = 8) -> "World":
+        h = ctypes.c_void_p()
+        _check(_lib().lsb_create_rank(ctypes.byref(h), n, num_ranks, rank, device, radix_bits,
+                                      unique_id), "lsb_create_rank")
+        return cls(n, _handle=h, _P=num_ranks, radix_bits=radix_bits)
+
+    # -- lifecycle --------------------------------------------------------
+    def close(self) -> None:
+        if self._h:
+            _lib().lsb_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_option(self, opt: int, value: int) -> None:
+        _check(_lib().lsb_set_option(self._h, opt, value), "lsb_set_option")
+
+    # -- data ---------------------------------------------------------------
+    def here(self, r: int) -> int:
+        return here(self.n, self.P, r)
+
+    def generate(self) -> None:
+        _check(_lib().lsb_generate(self._h), "lsb_generate")
+
+    def copy_in(self, rank: int, arr: np.ndarray, off: int = 0) -> None:
+        arr = np.ascontiguousarray(arr, dtype=ELEM_DTYPE)
+        _check(_lib().lsb_copy_in(self._h, rank, off, arr.size, arr.ctypes.data if arr.size else None),
+               "lsb_copy_in")
+
+    def copy_out(self, rank: int, off: int = 0, cnt: Optional[int] = None) -> np.ndarray:
+        if cnt is None:
+            cnt = self.here(rank) - off
+        out = np.empty(cnt, dtype=ELEM_DTYPE)
+        _check(_lib().lsb_copy_out(self._h, rank, off, cnt, out.ctypes.data if cnt else None),
+               "lsb_copy_out")
+        return out
+
+    def scatter_global(self, arr: np.ndarray) -> None:
+        """Load a global array of n records into the block partition."""
+        arr = np.ascontiguousarray(arr, dtype=ELEM_DTYPE)
+        if arr.size != self.n:
+            raise ValueError("need exactly n records")
+        for r in self.local_ranks:
+            h = self.here(r)
+            if h:
+                self.copy_in(r, arr[r * self.per: r * self.per + h])
+
+    def gather_global(self) -> np.ndarray:
+        """A[0:n] in global order (every rank must be local)."""
+        if len(self.local_ranks) != self.P:
+            raise RuntimeError("gather_global needs all ranks in this process")
+        parts = [self.copy_out(r) for r in range(self.P)]
+        return np.concatenate(parts) if parts else np.empty(0, dtype=ELEM_DTYPE)
+
+    # -- the hot path -------------------------------------------------------
+    def my_sort(self) -> None:
+        _check(_lib().lsb_sort(self._h), "lsb_sort")
+
+    def global_shuffle(self, digit: int) -> None:
+        _check(_lib().lsb_pass(self._h, digit), "lsb_pass")
+
+    mySort = my_sort
+    globalShuffle = global_shuffle
+
+    def sync(self) -> None:
+        _check(_lib().lsb_sync(self._h), "lsb_sync")
+
+    def barrier(self) -> None:
+        _check(_lib().lsb_barrier(self._h), "lsb_barrier")
+
+    # -- checks ---------------------------------------------------------------
+    def verify(self):
+        """(ok, first_bad_global_index) of the O(n) stable-sort invariant."""
+        bad = ctypes.c_int64(-1)
+        rc = _lib().lsb_verify(self._h, ctypes.byref(bad))
+        if rc not in (LSB_OK, LSB_ERR_VERIFY):
+            _check(rc, "lsb_verify")
+        return rc == LSB_OK, int(bad.value)
+
+    def check_sorted(self) -> bool:
+        s = ctypes.c_int(0)
+        _check(_lib().lsb_check_sorted(self._h, ctypes.byref(s)), "lsb_check_sorted")
+        return bool(s.value)
+
+    checkSorted = check_sorted
+
+    def print_lines(self, name: str = "A", n_per_rank: int = 10):
+        """The lines DistributedArray::print emits (mpi/mpi_lsbsort.cpp:171-200)."""
+        lines = []
+        if n_per_rank * self.P >= self.n:
+            lines.append(f"{name}: displaying all {self.n} elements")
+        else:
+            lines.append(f"{name}: displaying first {n_per_rank} elements on each rank"
+                         f" out of {self.n} elements")
+        for r in self.local_ranks:
+            h = self.here(r)
+            k = min(n_per_rank, h)
+            for i, e in enumerate(self.copy_out(r, 0, k)):
+                lines.append(f"{name}[{r * self.per + i}] = ({int(e['key']):016x},{int(e['val'])})")
+            if k < h:
+                lines.append("...")
+        return lines
+
+    # -- measurement ----------------------------------------------------------
+    def set_timing(self, on: bool = True) -> None:
+        self.set_option(OPT_TIMING, 1 if on else 0)
+
+    def kernel_stats(self) -> dict:
+        out = {}
+        for kid, name in enumerate(KERNEL_NAMES):
+            n = ctypes.c_int64()
+            ms = ctypes.c_double()
+            _check(_lib().lsb_get_kernel_stats(self._h, kid, ctypes.byref(n), ctypes.byref(ms)),
+                   "lsb_get_kernel_stats")
+            out[name] = (int(n.value), float(ms.value))
+        return out
+
+    def reset_kernel_stats(self) -> None:
+        _check(_lib().lsb_reset_kernel_stats(self._h), "lsb_reset_kernel_stats")
+
+    def scatter_elems(self) -> int:
+        e = ctypes.c_int64()
+        _check(_lib().lsb_get_scatter_elems(self._h, ctypes.byref(e)), "lsb_get_scatter_elems")
+        return int(e.value)
+
+
+def mySort(world: World) -> None:  # noqa: N802 - reference name
+    world.my_sort()
+
+
+def globalShuffle(world: World, digit: int) -> None:  # noqa: N802 - reference name
+    world.global_shuffle(digit)

@@ -1,0 +1,156 @@
+/*
+ * lsb.h — C ABI of the MI355X-native distributed LSD radix sort.
+ *
+ * The reference (ronawho/distributed-lsb) has no library or FFI: every
+ * variant is one program whose in-process seams are
+ *   mySort(A, B)              mpi/mpi_lsbsort.cpp:580-585, shmem/shmem_lsbsort.cpp:460-472
+ *   globalShuffle(A, B, d)    mpi/mpi_lsbsort.cpp:481-577, shmem/shmem_lsbsort.cpp:388-457
+ *   DistributedArray::create  mpi/mpi_lsbsort.cpp:137-161
+ *   checkSorted()             shmem/shmem_lsbsort.cpp:180-219
+ *   PCG input init            mpi/mpi_lsbsort.cpp:643-666
+ *   verify (gather + stable_sort + ==)  mpi/mpi_lsbsort.cpp:673-679,710-738
+ * Each entry point below names the seam it replaces.  Plain C types only;
+ * no C++ exception crosses this boundary; every function returning int
+ * returns LSB_OK (0) or an LSB_ERR_* code (lsb_strerror() describes it).
+ *
+ * A context is one "world" of P ranks (P = num_ranks) over the block
+ * partition per = ceil(n/P) (mpi/mpi_lsbsort.cpp:144-149):
+ *   - lsb_create():      one process drives all P ranks (logical ranks, each
+ *                        with its own buffers; several may share one GPU).
+ *                        The per-pass exchange is a device-to-device copy
+ *                        with exactly the all-to-all-v semantics of RCCL.
+ *   - lsb_create_rank(): one process per GPU (torchrun / hip_lsbsort --gpus);
+ *                        this process is rank `rank`; the exchange is RCCL
+ *                        (AllGather of bucket counts + grouped Send/Recv)
+ *                        over xGMI.  Collective calls must be made by all
+ *                        ranks in the same order, as in the MPI reference.
+ * The context owns every device buffer (A, B, send/recv, histograms, RCCL
+ * communicator), as DistributedArray owns localPart_.  A context is driven
+ * by one host thread and is not re-entrant.
+ */
+#ifndef LSB_H
+#define LSB_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LSB_OK                 0
+#define LSB_ERR_INVALID        1  /* bad argument (rank, range, digit, radix) */
+#define LSB_ERR_HIP            2  /* a HIP runtime call failed */
+#define LSB_ERR_RCCL           3  /* an RCCL call failed */
+#define LSB_ERR_NOMEM          4  /* device or host allocation failed */
+#define LSB_ERR_VERIFY         5  /* lsb_verify found a mismatch */
+#define LSB_ERR_UNSUPPORTED    6  /* valid request this build does not do */
+#define LSB_ERR_STATE          7  /* call not valid in this context state */
+
+#define LSB_UNIQUE_ID_BYTES  128  /* == NCCL_UNIQUE_ID_BYTES */
+
+/* == struct SortElement (mpi/mpi_lsbsort.cpp:29-32): 16 B, little-endian,
+ * key then val, no padding.  Order of the sort: key only, stable. */
+typedef struct lsb_elem {
+  uint64_t key;
+  uint64_t val;
+} lsb_elem_t;
+
+typedef struct lsb_ctx lsb_ctx_t;
+
+/* Kernel / phase ids for lsb_get_kernel_stats(). */
+#define LSB_K_UPSWEEP   0  /* per-chunk digit histogram (count)           */
+#define LSB_K_SCAN      1  /* chunk x bucket exclusive scan               */
+#define LSB_K_SCATTER   2  /* stable LDS-staged scatter (shuffle)         */
+#define LSB_K_EXCHANGE  3  /* bucket-count allgather + element all-to-all */
+#define LSB_K_PLACE     4  /* received runs -> final local slots          */
+#define LSB_K_SORT      5  /* whole lsb_sort()                            */
+#define LSB_K_COUNT     6
+
+/* Options for lsb_set_option(). */
+#define LSB_OPT_TIMING          0  /* 1: record HIP events around every kernel */
+#define LSB_OPT_FORCE_EXCHANGE  1  /* 1: run the exchange path even when P == 1 */
+
+/* ---- geometry: DistributedArray::create (mpi/mpi_lsbsort.cpp:144-149) ---- */
+int64_t lsb_per_rank(int64_t n_total, int num_ranks);            /* ceil(n/P) */
+int64_t lsb_here(int64_t n_total, int num_ranks, int rank);      /* clamp(n - r*per, 0, per) */
+
+/* ---- lifecycle ---------------------------------------------------------- */
+/* One process, `num_ranks` logical ranks; rank r lives on device dev_ids[r]
+ * (dev_ids == NULL: every rank on device 0).  radix_bits must be 8. */
+int  lsb_create(lsb_ctx_t** ctx, int64_t n_total, int num_ranks,
+                const int* dev_ids, int radix_bits);
+/* RCCL bootstrap: rank 0 calls this and ships the bytes to the other ranks
+ * (bench.py uses torch.distributed; hip_lsbsort uses a pipe). */
+int  lsb_get_unique_id(unsigned char id[LSB_UNIQUE_ID_BYTES]);
+/* One process per GPU: this process is `rank` of `num_ranks`, on `dev_id`. */
+int  lsb_create_rank(lsb_ctx_t** ctx, int64_t n_total, int num_ranks, int rank,
+                     int dev_id, int radix_bits,
+                     const unsigned char id[LSB_UNIQUE_ID_BYTES]);
+void lsb_destroy(lsb_ctx_t* ctx);
+int  lsb_set_option(lsb_ctx_t* ctx, int option, int64_t value);
+/* Ranks owned by this context: [*first_rank, *first_rank + *num_local). */
+int  lsb_local_ranks(const lsb_ctx_t* ctx, int* first_rank, int* num_local);
+
+/* ---- data --------------------------------------------------------------- */
+/* PCG input init (mpi/mpi_lsbsort.cpp:650-656), on device: for every local
+ * rank r and every one of its `per` slots i: key = i-th output of pcg64(r),
+ * val = r*per + i.  Untimed in the reference; untimed here. */
+int  lsb_generate(lsb_ctx_t* ctx);
+/* Host <-> A of a local rank, slots [off, off+cnt) of that rank's per slots. */
+int  lsb_copy_in(lsb_ctx_t* ctx, int rank, int64_t off, int64_t cnt, const lsb_elem_t* host);
+int  lsb_copy_out(lsb_ctx_t* ctx, int rank, int64_t off, int64_t cnt, lsb_elem_t* host);
+
+/* ---- the hot path ------------------------------------------------------- */
+/* == mySort(A, B): all 64/radix_bits passes; result in A.  Asynchronous
+ * with respect to the host except for the per-pass count exchange when
+ * P > 1; call lsb_sync() to wait. */
+int  lsb_sort(lsb_ctx_t* ctx);
+/* == globalShuffle(A, B, digit): one pass, result in A. */
+int  lsb_pass(lsb_ctx_t* ctx, int digit);
+int  lsb_sync(lsb_ctx_t* ctx);
+/* lsb_sync, then (RCCL contexts) a device all-reduce across the ranks:
+ * the MPI_Barrier around the timed region (mpi/mpi_lsbsort.cpp:688,693). */
+int  lsb_barrier(lsb_ctx_t* ctx);
+
+/* ---- checks ------------------------------------------------------------- */
+/* Bit-exact check equivalent to the MPI verify (stable_sort + ==), in O(n)
+ * on device, valid for PCG input from lsb_generate(): for every global i,
+ * out[i].val < n, out[i].key == pcg64(val / per)[val % per] and
+ * (key, val)[i] < (key, val)[i+1] strictly, across rank boundaries too.
+ * Returns LSB_OK when all hold, LSB_ERR_VERIFY otherwise; *first_bad gets
+ * the smallest failing global index (or -1). */
+int  lsb_verify(lsb_ctx_t* ctx, int64_t* first_bad);
+/* == checkSorted (shmem/shmem_lsbsort.cpp:180-219): key order inside every
+ * rank and across rank boundaries.  *sorted = 1 / 0. */
+int  lsb_check_sorted(lsb_ctx_t* ctx, int* sorted);
+
+/* ---- measurement -------------------------------------------------------- */
+/* With LSB_OPT_TIMING on: launches recorded and their summed device time
+ * (HIP events on the stream each kernel runs on) since the last reset. */
+int  lsb_get_kernel_stats(lsb_ctx_t* ctx, int kernel_id, int64_t* launches, double* total_ms);
+int  lsb_reset_kernel_stats(lsb_ctx_t* ctx);
+/* Elements one launch of the scatter kernel processed, summed like the stats. */
+int  lsb_get_scatter_elems(lsb_ctx_t* ctx, int64_t* elems);
+
+/* ---- host planner (pure host code; used by the runtime when P > 1) ------- */
+/* Given hist[s*nbuckets + b] = number of elements of bucket b that rank s
+ * holds after its local stable pass (bucket order), compute rank `rank`'s
+ * side of the exchange under the digit-major, rank-minor global order of
+ * copyCountsToGlobalCounts / exclusiveScan (mpi/mpi_lsbsort.cpp:350,378,401):
+ *   send_counts[q], send_displs[q]  elements of my bucket-ordered buffer for q
+ *   recv_counts[s], recv_displs[s]  elements arriving from s, in s order
+ *   place_off[s*nbuckets + b]       local slot = place_off[s][b] + recv index
+ * All arrays are caller-allocated (P or P*nbuckets int64). */
+int  lsb_plan_exchange(int64_t n_total, int num_ranks, int rank, int nbuckets,
+                       const int64_t* hist,
+                       int64_t* send_counts, int64_t* send_displs,
+                       int64_t* recv_counts, int64_t* recv_displs,
+                       int64_t* place_off);
+
+const char* lsb_strerror(int code);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LSB_H */

@@ -1,0 +1,250 @@
+"""Parity of the HIP path against the oracle and the reference's own outputs.
+
+Everything here calls through the C ABI (build/liblsb.so) on the GPU.
+Bar: bit-exact (integer / index work).  Multi-rank cases run P logical ranks
+on one GPU (lsb_create): the same kernels, plan and placement as the RCCL
+path, with the all-to-all done by device copies — the single-GPU analogue of
+`mpirun -n P mpi_lsbsort` on one host.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+DT = np.dtype([("key", "<u8"), ("val", "<u8")])
+
+
+def _records(rows):
+    a = np.zeros(len(rows), dtype=DT)
+    for i, r in enumerate(rows):
+        a[i] = (int(r[1], 16), r[2])
+    return a
+
+
+def _sorted_world(lsbsort, arr, P):
+    w = lsbsort.World(arr.size, ranks=P)
+    w.scatter_global(arr)
+    w.my_sort()
+    out = w.gather_global()
+    return w, out
+
+
+# --------------------------------------------------------------- generation
+@pytest.mark.parametrize("n,P", [(1, 1), (20, 2), (4097, 1), (100_003, 4), (17, 8), (3, 4)])
+def test_generate_matches_reference_input(lsb_built, oracle_mod, n, P):
+    with lsb_built.World(n, ranks=P) as w:
+        w.generate()
+        assert np.array_equal(w.gather_global(), oracle_mod.generate(n, P))
+
+
+# --------------------------------------------------------------- golden rows
+@pytest.mark.parametrize("row", range(5))
+def test_golden_digests(lsb_built, oracle_mod, digests, row):
+    d = digests["rows"][row]
+    with lsb_built.World(d["n"], ranks=d["P"]) as w:
+        w.generate()
+        assert oracle_mod.digest(w.gather_global()) == d["input"]
+        w.my_sort()
+        assert oracle_mod.digest(w.gather_global()) == d["output"]
+        ok, bad = w.verify()
+        assert ok and bad == -1
+        assert w.check_sorted()
+
+
+def test_reference_print_vectors(lsb_built, ref_vectors):
+    for case in ref_vectors["cases"]:
+        n, P = case["n"], case["P"]
+        with lsb_built.World(n, ranks=P) as w:
+            w.generate()
+            before = w.gather_global()
+            w.my_sort()
+            after = w.gather_global()
+            for rows, arr in ((case["input"], before), (case["output"], after)):
+                idx = [r[0] for r in rows]
+                np.testing.assert_array_equal(arr[idx], _records(rows))
+
+
+def test_print_lines_match_reference_format(lsb_built, ref_vectors):
+    case = next(c for c in ref_vectors["cases"] if c["n"] == 20 and c["P"] == 2)
+    with lsb_built.World(20, ranks=2) as w:
+        w.generate()
+        w.my_sort()
+        lines = w.print_lines("A", 10)
+    assert lines[0] == "A: displaying all 20 elements"
+    expect = [f"A[{i}] = ({k},{v})" for i, k, v in case["output"]]
+    assert lines[1:] == expect
+
+
+# ------------------------------------------------------------- single pass
+@pytest.mark.parametrize("n", [1, 63, 4095, 4096, 4097, 300_001])
+def test_single_pass_matches_local_shuffle(lsb_built, oracle_mod, n):
+    rng = np.random.default_rng(n)
+    a = np.zeros(n, dtype=DT)
+    a["key"] = rng.integers(0, 2**63, n, dtype=np.uint64) * np.uint64(2) + rng.integers(0, 2, n, dtype=np.uint64)
+    a["val"] = np.arange(n, dtype=np.uint64)
+    with lsb_built.World(n, ranks=1) as w:
+        w.copy_in(0, a)
+        cur = a
+        for d in (0, 3, 7):
+            w.global_shuffle(d)
+            cur, _ = oracle_mod.local_pass(cur, 8, d)
+            assert np.array_equal(w.copy_out(0), cur)
+
+
+# ------------------------------------------------------- adversarial inputs
+def _dist(name, n, rng):
+    a = np.zeros(n, dtype=DT)
+    a["val"] = np.arange(n, dtype=np.uint64)
+    if name == "all_equal":
+        a["key"] = np.uint64(0xDEADBEEF12345678)
+    elif name == "two_keys":
+        a["key"] = np.where(rng.random(n) < 0.5, 7, 0xFFFFFFFFFFFFFFFF).astype(np.uint64)
+    elif name == "hot_bucket":
+        k = rng.integers(0, 2**64 - 1, n, dtype=np.uint64)
+        hot = rng.random(n) < 0.9
+        k[hot] = (k[hot] & ~np.uint64(0xFF00FF)) | np.uint64(0x2A002A)
+        a["key"] = k
+    elif name == "high_bits_only":
+        a["key"] = rng.integers(0, 256, n, dtype=np.uint64) << np.uint64(56)
+    elif name == "zipf":
+        z = np.minimum(rng.zipf(1.1, n), 2**20).astype(np.uint64)
+        a["key"] = z * np.uint64(0x9E3779B97F4A7C15)  # spread over all digits
+    elif name == "sorted":
+        a["key"] = np.sort(rng.integers(0, 2**64 - 1, n, dtype=np.uint64))
+    elif name == "reverse":
+        a["key"] = np.sort(rng.integers(0, 2**64 - 1, n, dtype=np.uint64))[::-1]
+    elif name == "small_range":
+        a["key"] = rng.integers(0, 3, n, dtype=np.uint64)
+    else:
+        raise KeyError(name)
+    return a
+
+
+@pytest.mark.parametrize("name", ["all_equal", "two_keys", "hot_bucket", "high_bits_only",
+                                  "zipf", "sorted", "reverse", "small_range"])
+@pytest.mark.parametrize("P", [1, 3, 8])
+def test_distributions_bit_exact(lsb_built, oracle_mod, name, P):
+    rng = np.random.default_rng(hash((name, P)) & 0xFFFF)
+    n = 200_003
+    a = _dist(name, n, rng)
+    _, out = _sorted_world(lsb_built, a, P)
+    assert np.array_equal(out, oracle_mod.stable_sort(a))
+
+
+@pytest.mark.parametrize("n,P", [(0, 1), (0, 3), (1, 1), (1, 4), (2, 8), (5, 8), (9, 8),
+                                 (4096 * 3 + 1, 2), (4096 * 513 + 7, 1)])
+def test_ragged_and_tiny(lsb_built, oracle_mod, n, P):
+    rng = np.random.default_rng(n * 31 + P)
+    a = np.zeros(n, dtype=DT)
+    a["key"] = rng.integers(0, 2**64 - 1, n, dtype=np.uint64) & np.uint64(0xF0F0F0F0F0F0F0F0)
+    a["val"] = np.arange(n, dtype=np.uint64)
+    _, out = _sorted_world(lsb_built, a, P)
+    assert np.array_equal(out, oracle_mod.stable_sort(a))
+
+
+# ------------------------------------------------------------------ checks
+def test_verify_catches_corruption(lsb_built):
+    n, P = 100_000, 2
+    with lsb_built.World(n, ranks=P) as w:
+        w.generate()
+        w.my_sort()
+        assert w.verify() == (True, -1)
+        part = w.copy_out(1, 0, 8)
+        part[[3, 4]] = part[[4, 3]]  # breaks order at global per+3
+        w.copy_in(1, part, 0)
+        ok, bad = w.verify()
+        assert not ok and bad == w.per + 3
+        assert not w.check_sorted()
+        part[[3, 4]] = part[[4, 3]]
+        part[5]["val"] ^= 1  # key no longer PCG(val): stable order broken
+        w.copy_in(1, part, 0)
+        ok, bad = w.verify()
+        assert not ok and bad in (w.per + 4, w.per + 5)
+        assert w.check_sorted()  # keys still in order
+
+
+def test_check_sorted_rank_boundary(lsb_built):
+    n, P = 10_000, 4
+    with lsb_built.World(n, ranks=P) as w:
+        w.generate()
+        w.my_sort()
+        last = w.copy_out(0, w.per - 1, 1)
+        first = w.copy_out(1, 0, 1)
+        w.copy_in(0, first, w.per - 1)
+        w.copy_in(1, last, 0)
+        assert not w.check_sorted()
+
+
+# ------------------------------------------------------- exchange / RCCL paths
+def test_forced_exchange_at_p1(lsb_built, oracle_mod, digests):
+    d = next(r for r in digests["rows"] if r["P"] == 1)
+    with lsb_built.World(d["n"], ranks=1) as w:
+        w.set_option(lsb_built.OPT_FORCE_EXCHANGE, 1)
+        w.generate()
+        w.my_sort()
+        assert oracle_mod.digest(w.gather_global()) == d["output"]
+
+
+def test_rccl_world_of_one(lsb_built, oracle_mod, digests):
+    d = next(r for r in digests["rows"] if r["P"] == 1)
+    uid = lsb_built.get_unique_id()
+    w = lsb_built.World.rank(d["n"], 1, 0, 0, uid)
+    try:
+        w.set_option(lsb_built.OPT_FORCE_EXCHANGE, 1)
+        w.generate()
+        w.barrier()
+        w.my_sort()
+        w.barrier()
+        assert oracle_mod.digest(w.copy_out(0)) == d["output"]
+        assert w.verify() == (True, -1)
+        assert w.check_sorted()
+    finally:
+        w.close()
+
+
+def test_kernel_stats(lsb_built):
+    with lsb_built.World(1 << 20, ranks=1) as w:
+        w.generate()
+        w.set_timing(True)
+        w.my_sort()
+        st = w.kernel_stats()
+        assert st["scatter"][0] == 8 and st["upsweep"][0] == 8 and st["sort"][0] == 1
+        assert st["scatter"][1] > 0
+        assert w.scatter_elems() == 8 << 20
+
+
+# ------------------------------------------------------------ larger sizes
+@pytest.mark.parametrize("n,P", [(1 << 27, 1), ((1 << 26) + 12345, 2)])
+def test_large_verify_on_device(lsb_built, n, P):
+    with lsb_built.World(n, ranks=P) as w:
+        w.generate()
+        w.my_sort()
+        assert w.verify() == (True, -1)
+        assert w.check_sorted()
+
+
+# ------------------------------------------------------------- the harness
+def test_harness_matches_reference_lines(lsb_built, ref_vectors):
+    case = next(c for c in ref_vectors["cases"] if c["n"] == 1000003 and c["P"] == 4)
+    exe = lsb_built.HARNESS_PATH
+    out = subprocess.run([exe, "--n", "1000003", "--ranks", "4", "--print"], check=True,
+                         capture_output=True, text=True, timeout=300).stdout
+    lines = out.splitlines()
+    assert lines[0] == "Total number of HIP ranks: 4"
+    assert lines[1] == "Problem size: 1000003"
+    assert "Verifying" in lines and "Array is sorted" in lines
+    assert any(l.startswith("That's ") and l.endswith(" M elements sorted / s") for l in lines)
+    printed = [l for l in lines if l.startswith("A[")]
+    expect = [f"A[{i}] = ({k},{v})" for i, k, v in case["input"] + case["output"]]
+    assert printed == expect
+
+
+def test_harness_one_gpu_process(lsb_built):
+    exe = lsb_built.HARNESS_PATH
+    r = subprocess.run([exe, "--n", "300000", "--gpus", "1", "--verify", "--json"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert "Array is sorted" in r.stdout
