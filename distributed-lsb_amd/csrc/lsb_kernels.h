@@ -19,7 +19,7 @@ constexpr int kBuckets = 1 << kDigitBits;     // 256
 constexpr int kScatterBlock = 256;            // 4 waves
 constexpr int kScatterIpt = 16;               // items per thread
 constexpr int kTile = kScatterBlock * kScatterIpt;  // 4096 elements = 64 KiB in LDS
-constexpr int kMaxChunks = 1024;              // upper bound on the chunk grid
+constexpr int kMaxChunks = 65536;             // upper bound on the chunk grid
 
 // A rank's `m` elements are cut into `num_chunks` contiguous chunks of
 // `chunk_elems` (a multiple of kTile; the last may be short).  The count

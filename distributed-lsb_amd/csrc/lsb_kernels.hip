@@ -183,31 +183,37 @@ __global__ __launch_bounds__(BLOCK) void k_upsweep(const Elem* __restrict__ A, i
 
 // -------------------------------------------------------------------- scan
 constexpr int kScanBlock = 256;
-constexpr int kScanPer = kMaxChunks / kScanBlock;  // 4
+constexpr int kScanPer = 4;  // one segment = 1024 chunks
 
+// One workgroup per bucket row; the row is scanned in segments of
+// kScanBlock * kScanPer chunks with a running carry.
 __global__ __launch_bounds__(kScanBlock) void k_scan(const uint32_t* __restrict__ chunk_hist,
                                                      int G, uint64_t* __restrict__ chunk_off,
                                                      uint64_t* __restrict__ totals) {
   __shared__ uint64_t tmp[kScanBlock / 64];
   const int b = blockIdx.x;
   const uint32_t* row = chunk_hist + (int64_t)b * G;
-  uint32_t v[kScanPer];
-  uint64_t sum = 0;
+  uint64_t carry = 0;
+  for (int seg = 0; seg < G; seg += kScanBlock * kScanPer) {
+    uint32_t v[kScanPer];
+    uint64_t sum = 0;
 #pragma unroll
-  for (int j = 0; j < kScanPer; ++j) {
-    const int c = threadIdx.x * kScanPer + j;
-    v[j] = c < G ? row[c] : 0u;
-    sum += v[j];
-  }
-  uint64_t total;
-  uint64_t pre = block_exclusive_scan<kScanBlock>(sum, tmp, &total);
+    for (int j = 0; j < kScanPer; ++j) {
+      const int c = seg + threadIdx.x * kScanPer + j;
+      v[j] = c < G ? row[c] : 0u;
+      sum += v[j];
+    }
+    uint64_t total;
+    uint64_t pre = carry + block_exclusive_scan<kScanBlock>(sum, tmp, &total);
 #pragma unroll
-  for (int j = 0; j < kScanPer; ++j) {
-    const int c = threadIdx.x * kScanPer + j;
-    if (c < G) chunk_off[(int64_t)b * G + c] = pre;
-    pre += v[j];
+    for (int j = 0; j < kScanPer; ++j) {
+      const int c = seg + threadIdx.x * kScanPer + j;
+      if (c < G) chunk_off[(int64_t)b * G + c] = pre;
+      pre += v[j];
+    }
+    carry += total;
   }
-  if (threadIdx.x == 0) totals[b] = total;
+  if (threadIdx.x == 0) totals[b] = carry;
 }
 
 // ----------------------------------------------------------------- scatter
@@ -215,6 +221,19 @@ __global__ __launch_bounds__(kScanBlock) void k_scan(const uint32_t* __restrict_
 // wave w owns tile elements [w*64*IPT, (w+1)*64*IPT) and its item i is the
 // 64 consecutive elements starting at w*64*IPT + i*64, so tile order is
 // (wave, item, lane) and every load is a coalesced 1 KiB wave-instruction.
+//
+// Whole-line writes.  A tile's run of bucket b starts at an arbitrary record,
+// so its first and last 128-B lines are shared with the previous and next
+// tile's runs.  Written ~20 us apart, such a line is usually evicted from L2
+// half-written and HBM pays for a partial-line write (measured: 256-B runs
+// misaligned by 16 B drop from 4.6 to 3.6 TB/s; tools/kbench/runs2.hip).
+// So a tile writes only [A_b, E_b) with E_b on a line boundary and keeps the
+// <= 7 records of its last, incomplete line in registers of thread b (the
+// "carry"); the next tile writes them in the same phase as the rest of that
+// line, and L2 merges the line before it leaves.  Only a chunk's first and
+// last line per bucket can still be partial.
+constexpr int kLineElems = 8;  // 128-B line / 16-B record
+
 template <int BLOCK, int IPT>
 __global__ __launch_bounds__(BLOCK, 2) void k_scatter(const Elem* __restrict__ in,
                                                       Elem* __restrict__ out, int64_t m,
@@ -223,11 +242,13 @@ __global__ __launch_bounds__(BLOCK, 2) void k_scatter(const Elem* __restrict__ i
                                                       const uint64_t* __restrict__ totals) {
   constexpr int W = BLOCK / 64;
   constexpr int T = BLOCK * IPT;
+  constexpr int CY = kLineElems - 1;
   static_assert(BLOCK >= kBuckets, "one thread per bucket in the offset phase");
 
   __shared__ Elem stage[T];                 // the ranked tile (64 KiB)
   __shared__ uint32_t wcnt[W][kBuckets];    // per-wave digit counters -> positions
   __shared__ int64_t delta[kBuckets];       // global dest = delta[digit] + tile position
+  __shared__ int64_t lim[kBuckets];         // write only dest < lim[digit] (E_b)
   __shared__ uint64_t scan64[W];
   __shared__ uint32_t scan32[W];
 
@@ -246,9 +267,15 @@ __global__ __launch_bounds__(BLOCK, 2) void k_scatter(const Elem* __restrict__ i
     const uint64_t bstart = block_exclusive_scan<BLOCK>(tot, scan64, &all);
     if (t < kBuckets) run = bstart + chunk_off[(int64_t)t * G + c];
   }
+  // Carry of bucket t (thread t < 256): records for dest [run - cy_len, run).
+  Elem cy[CY];
+  uint32_t cy_len = 0;
+#pragma unroll
+  for (int i = 0; i < CY; ++i) cy[i] = Elem{0ull, 0ull};
 
   for (int64_t tb = beg; tb < end; tb += T) {
     const int nvalid = (int)((end - tb) < T ? (end - tb) : T);
+    const bool last_tile = tb + T >= end;
 
 #pragma unroll
     for (int j = 0; j < kBuckets / 64; ++j) wcnt[w][lane + 64 * j] = 0;
@@ -287,11 +314,23 @@ __global__ __launch_bounds__(BLOCK, 2) void k_scatter(const Elem* __restrict__ i
     }
     uint32_t tile_total;
     const uint32_t lstart = block_exclusive_scan<BLOCK>(cnt, scan32, &tile_total);
+    // Run of bucket t in this tile: dest [R, R + cnt); carried [A, R).
+    // Write [A, E): E = end of the last whole line, or everything at the
+    // chunk's last tile; E == A means the line is still incomplete.
+    int64_t R = 0, A = 0, E = 0, run_end = 0;
+    bool flush_carry = false;
     if (t < kBuckets) {
 #pragma unroll
       for (int ww = 0; ww < W; ++ww) wcnt[ww][t] += lstart;
-      delta[t] = (int64_t)run - (int64_t)lstart;
-      run += cnt;
+      R = (int64_t)run;
+      A = R - (int64_t)cy_len;
+      run_end = R + cnt;
+      const int64_t aligned = run_end & ~(int64_t)(kLineElems - 1);
+      E = last_tile ? run_end : (aligned > A ? aligned : A);
+      flush_carry = E > A;
+      delta[t] = R - (int64_t)lstart;
+      lim[t] = E;
+      run = (uint64_t)run_end;
     }
     __syncthreads();
 
@@ -307,9 +346,29 @@ __global__ __launch_bounds__(BLOCK, 2) void k_scatter(const Elem* __restrict__ i
     for (int j = t; j < nvalid; j += BLOCK) {
       const Elem x = stage[j];
       const uint32_t d = (uint32_t)(x.key >> shift) & (kBuckets - 1);
-      store_elem(out + (delta[d] + j), x);
+      const int64_t g = delta[d] + j;
+      if (g < lim[d]) store_elem(out + g, x);
+    }
+    // The carried head of each line goes out in the same phase as its rest.
+    if (flush_carry) {
+#pragma unroll
+      for (int i = 0; i < CY; ++i)
+        if ((uint32_t)i < cy_len) store_elem(out + A + i, cy[i]);
     }
     __syncthreads();
+
+    // New carry: records for dest [E, run_end).  If nothing was written the
+    // old carry stays in front and this tile's records are appended.
+    if (t < kBuckets) {
+      const uint32_t keep = flush_carry ? 0u : cy_len;
+      const int64_t src0 = flush_carry ? (int64_t)lstart + (E - R) : (int64_t)lstart;
+      const uint32_t new_len = (uint32_t)(run_end - E);
+#pragma unroll
+      for (int i = 0; i < CY; ++i) {
+        if ((uint32_t)i >= keep && (uint32_t)i < new_len) cy[i] = stage[src0 + (i - (int)keep)];
+      }
+      cy_len = new_len;
+    }
   }
 }
 
