@@ -148,13 +148,20 @@ __global__ __launch_bounds__(256) void k_pcg_fill(Elem* __restrict__ A, int64_t 
 }
 
 // ----------------------------------------------------------------- upsweep
+// Per-wave LDS histograms with plain ds_add: on uniform digits this runs at
+// the pure-read rate (2.80 ms for 2^30 records = 6.1 TB/s, vs 3.57 ms with
+// ballot-match aggregation; tools/kbench/upsweep.hip).  A wave whose 64
+// digits are all equal (sorted or skewed input) adds once instead of
+// serialising 64 same-address atomics.
 template <int BLOCK, int IPT>
 __global__ __launch_bounds__(BLOCK) void k_upsweep(const Elem* __restrict__ A, int64_t m,
                                                    int shift, int64_t chunk_elems, int G,
                                                    uint32_t* __restrict__ chunk_hist) {
-  __shared__ uint32_t hist[kBuckets];
-  for (int b = threadIdx.x; b < kBuckets; b += BLOCK) hist[b] = 0;
+  constexpr int W = BLOCK / 64;
+  __shared__ uint32_t hist[W][kBuckets];
+  for (int i = threadIdx.x; i < W * kBuckets; i += BLOCK) (&hist[0][0])[i] = 0;
   __syncthreads();
+  const int w = threadIdx.x >> 6;
 
   const int c = blockIdx.x;
   const int64_t beg = (int64_t)c * chunk_elems;
@@ -173,12 +180,21 @@ __global__ __launch_bounds__(BLOCK) void k_upsweep(const Elem* __restrict__ A, i
       const int64_t idx = tb + (int64_t)i * BLOCK + threadIdx.x;
       const bool valid = idx < end;
       const uint32_t d = (uint32_t)(k[i] >> shift) & (kBuckets - 1);
-      const uint64_t mt = match_digit8(d, __ballot(valid));
-      if (valid && mbcnt(mt) == 0) atomicAdd(&hist[d], (uint32_t)__popcll(mt));
+      const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
+      if (__all(valid && d == d0)) {
+        if (lane_id() == 0) atomicAdd(&hist[w][d0], 64u);
+      } else if (valid) {
+        atomicAdd(&hist[w][d], 1u);
+      }
     }
   }
   __syncthreads();
-  for (int b = threadIdx.x; b < kBuckets; b += BLOCK) chunk_hist[(int64_t)b * G + c] = hist[b];
+  for (int b = threadIdx.x; b < kBuckets; b += BLOCK) {
+    uint32_t s = 0;
+#pragma unroll
+    for (int ww = 0; ww < W; ++ww) s += hist[ww][b];
+    chunk_hist[(int64_t)b * G + c] = s;
+  }
 }
 
 // -------------------------------------------------------------------- scan
