@@ -53,6 +53,11 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=1 << 27,
                     help="records the CPU baseline sorts (bounded sample)")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--radix-bits", type=int, default=0,
+                    help="exchange digit width: 8 or 16 (default: 8 on 1 GPU, 16 on >1 GPU; "
+                         "local passes are 8-bit either way)")
+    ap.add_argument("--dist", choices=("uniform", "zipf"), default="uniform")
+    ap.add_argument("--zipf-s", type=float, default=1.1)
     return ap.parse_args()
 
 
@@ -101,13 +106,26 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def device_sync():
+_TORCH_DEV = None
+
+
+def bind_device(local_rank):
+    """Point torch at this rank's GPU so its synchronize() waits on that device."""
+    global _TORCH_DEV
     try:
         import torch
         if torch.cuda.is_available():
-            torch.cuda.synchronize()
+            torch.cuda.set_device(local_rank)
+            _TORCH_DEV = local_rank
     except Exception:
-        pass
+        _TORCH_DEV = None
+
+
+def device_sync():
+    if _TORCH_DEV is None:
+        return
+    import torch
+    torch.cuda.synchronize(_TORCH_DEV)
 
 
 def load_traffic(workload):
@@ -163,17 +181,19 @@ def main():
     if d.world > 1 and a.gpus != d.world:
         N = d.world
     n_total = a.n_per_gpu * N
+    radix = a.radix_bits or (8 if N == 1 else 16)
     if d.world > 1:
         uid = lsbsort.get_unique_id() if d.rank == 0 else None
         uid = d.bcast_bytes(uid)
-        w = lsbsort.World.rank(n_total, N, d.rank, d.local_rank, uid)
+        w = lsbsort.World.rank(n_total, N, d.rank, d.local_rank, uid, radix_bits=radix)
     else:
         if N != 1:
             raise SystemExit("multi-GPU runs are launched one process per GPU (torch.distributed.run)")
-        w = lsbsort.World(n_total, ranks=1)
+        w = lsbsort.World(n_total, ranks=1, radix_bits=radix)
+    bind_device(d.local_rank)
 
     def step(timed):
-        w.generate()
+        w.generate(a.dist, a.zipf_s)
         w.barrier()
         device_sync()
         d.barrier()
@@ -203,7 +223,13 @@ def main():
     ms_per_step = total / a.steps * 1e3
     value = n_total * a.steps / total / 1e6
     launches, scatter_ms = stats["scatter"]
-    workload = f"configs[1]: sort of 2^30 16-byte records per GPU, 8-bit digits, 8 passes, {N} GPU(s)"
+    if N == 1:
+        workload = f"configs[1]: sort of 2^30 16-byte records per GPU, 8-bit digits, 8 passes, {N} GPU(s)"
+    else:
+        workload = (f"configs[2]: sort of {N} x 2^30 16-byte records block-partitioned over {N} GPUs, "
+                    f"8-bit local passes, {radix}-bit exchange digits ({64 // radix} RCCL all-to-alls)")
+    if a.dist != "uniform":
+        workload += f", zipf s={a.zipf_s} keys"
     roof = None
     if launches and scatter_ms > 0:
         elems_per_launch = scatter_elems / launches
@@ -227,10 +253,13 @@ def main():
         "scaling": "weak",
         "vs_baseline": round(value / REF_MPI_MELEMS, 3),
         "dtype": "u64",
-        "data": "synthetic: pcg64(rank) keys, val = global index (mpi_lsbsort.cpp:650-656), regenerated on device before every step",
+        "data": ("synthetic: pcg64(rank) keys, val = global index (mpi_lsbsort.cpp:650-656), regenerated on device before every step"
+                 if a.dist == "uniform" else
+                 f"synthetic: zipf(s={a.zipf_s}) keys drawn from the pcg64(rank) stream (build-defined, SURVEY 8d C4)"),
         "config": {"workload": workload, "n_total": n_total, "n_per_gpu": a.n_per_gpu,
-                   "radix_bits": 8, "passes": 8, "record_bytes": 16,
-                   "parallelism": f"block partition over {N} GPU(s); per pass RCCL AllGather of counts + Send/Recv all-to-all" if N > 1 else "1 GPU, no exchange"},
+                   "local_digit_bits": 8, "local_passes": 8, "exchange_digit_bits": radix if N > 1 else None,
+                   "record_bytes": 16, "dist": a.dist,
+                   "parallelism": f"block partition over {N} GPU(s); per exchange digit RCCL AllGather of counts + Send/Recv all-to-all" if N > 1 else "1 GPU, no exchange"},
         "roofline": roof,
         "sort_hbm_frac": round(sort_gbs / HBM_PEAK_GBS, 4),
         "kernel_ms_per_step": {k: round(v[1] / a.steps, 3) for k, v in stats.items()},

@@ -32,8 +32,24 @@ struct Chunking {
 };
 Chunking make_chunking(int64_t m, int max_chunks);
 
-// On-device PCG64 (pcg-cpp setseq_xsl_rr_128_64): A[i] = {pcg64(seed)[i], val0 + i}.
-hipError_t launch_pcg_fill(Elem* A, int64_t count, uint64_t seed, uint64_t val0, hipStream_t s);
+// Input distribution of lsb_generate_ex: the key made from the PCG draw.
+constexpr int kDistUniform = 0;  // key = draw (the reference's input)
+constexpr int kDistZipf = 1;     // key = mix64(Zipf-like rank of the draw), SURVEY §8d C4
+struct KeyGen {
+  int dist = kDistUniform;
+  double zipf_s = 1.1;
+  uint64_t zipf_n = 1ull << 30;
+};
+
+// On-device PCG64 (pcg-cpp setseq_xsl_rr_128_64):
+// A[i] = {make_key(pcg64(seed)[i]), val0 + i}.
+hipError_t launch_pcg_fill(Elem* A, int64_t count, uint64_t seed, uint64_t val0, KeyGen gen,
+                           hipStream_t s);
+
+// 65536-bin histogram of the 16-bit digit at `shift` of records already
+// sorted by that digit (first[] is 65536 int64 scratch).
+hipError_t launch_digit16_counts(const Elem* A, int64_t m, int shift, int64_t* first,
+                                 uint64_t* counts, hipStream_t s);
 
 // chunk_hist[b * G + c] = number of elements of chunk c whose digit is b.
 hipError_t launch_upsweep(const Elem* A, int64_t m, int shift, Chunking ch,
@@ -50,14 +66,14 @@ hipError_t launch_scatter(const Elem* in, Elem* out, int64_t m, int shift, Chunk
                           const uint64_t* chunk_off, const uint64_t* totals, hipStream_t s);
 
 // Receiver-side placement after the exchange: recv[k] (from source s, the
-// first s with k < rend[s]) goes to A[place_off[s * 256 + digit] + k].
-hipError_t launch_place(const Elem* recv, Elem* A, int64_t m, int shift, int P,
+// first s with k < rend[s]) goes to A[place_off[s * nbuckets + digit] + k].
+hipError_t launch_place(const Elem* recv, Elem* A, int64_t m, int shift, int nbuckets, int P,
                         const int64_t* rend, const int64_t* place_off, hipStream_t s);
 
 // O(n) bit-exact stable-sort check of a rank's here-part (see lsb_verify).
 // first_bad must hold UINT64_MAX before the launch; receives min bad global index.
 hipError_t launch_verify(const Elem* A, int64_t here, int64_t gbase, int64_t n, int64_t per,
-                         unsigned long long* first_bad, hipStream_t s);
+                         KeyGen gen, unsigned long long* first_bad, hipStream_t s);
 
 // Key-only local sortedness (checkSorted); *unsorted set to 1 on a descent.
 hipError_t launch_check_sorted(const Elem* A, int64_t here, unsigned int* unsorted, hipStream_t s);

@@ -135,15 +135,44 @@ __device__ __forceinline__ T block_exclusive_scan(T v, T* tmp, T* total) {
 // ---------------------------------------------------------------- PCG fill
 constexpr int kFillPerThread = 16;
 
+// splitmix64 finalizer: a bijection on 64-bit words.
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// Key of a record from its PCG draw.  Uniform: the draw itself (the
+// reference's input).  Zipf (build-defined): rank
+// k = floor(x) of a continuous power law on [1, N+1) with exponent s, by
+// inverse CDF from u = top 53 bits of the draw; key = mix64(k), so every
+// digit is skewed and duplicate keys are heavy.
+__device__ __forceinline__ uint64_t make_key(uint64_t draw, const KeyGen& g) {
+  if (g.dist == kDistUniform) return draw;
+  const double u = (double)(draw >> 11) * 0x1.0p-53;  // [0, 1)
+  const double n1 = (double)g.zipf_n + 1.0;
+  double x;
+  if (g.zipf_s == 1.0) {
+    x = exp(u * log(n1));
+  } else {
+    const double e = 1.0 - g.zipf_s;
+    x = pow(1.0 - u * (1.0 - pow(n1, e)), 1.0 / e);
+  }
+  uint64_t k = (uint64_t)x;
+  if (k < 1) k = 1;
+  if (k > g.zipf_n) k = g.zipf_n;
+  return mix64(k);
+}
+
 __global__ __launch_bounds__(256) void k_pcg_fill(Elem* __restrict__ A, int64_t count,
-                                                  uint64_t seed, uint64_t val0) {
+                                                  uint64_t seed, uint64_t val0, KeyGen g) {
   const int64_t first = ((int64_t)blockIdx.x * 256 + threadIdx.x) * kFillPerThread;
   if (first >= count) return;
   u128 s = pcg_jump(pcg_seed(seed), (uint64_t)first);
   const int64_t last = first + kFillPerThread < count ? first + kFillPerThread : count;
   for (int64_t i = first; i < last; ++i) {
     s = s * kPcgMult + kPcgInc;  // operator(): bump, then output the new state
-    store_elem(A + i, Elem{pcg_output(s), val0 + (uint64_t)i});
+    store_elem(A + i, Elem{make_key(pcg_output(s), g), val0 + (uint64_t)i});
   }
 }
 
@@ -390,19 +419,21 @@ __global__ __launch_bounds__(BLOCK, 2) void k_scatter(const Elem* __restrict__ i
 
 // ------------------------------------------------------------------- place
 constexpr int kPlaceBlock = 256;
-constexpr int kPlaceLdsRanks = 16;  // P * 256 offsets (32 KiB) staged in LDS up to here
+constexpr int kPlaceLdsEntries = 4096;  // P * nbuckets offsets (32 KiB) staged in LDS up to here
 
 template <bool kLds>
 __global__ __launch_bounds__(kPlaceBlock) void k_place(const Elem* __restrict__ recv,
                                                        Elem* __restrict__ A, int64_t m, int shift,
-                                                       int P, const int64_t* __restrict__ rend,
+                                                       uint32_t mask, int P,
+                                                       const int64_t* __restrict__ rend,
                                                        const int64_t* __restrict__ place_off) {
-  __shared__ int64_t lds_off[kLds ? kPlaceLdsRanks * kBuckets : 1];
-  __shared__ int64_t lds_end[kLds ? kPlaceLdsRanks : 1];
+  __shared__ int64_t lds_off[kLds ? kPlaceLdsEntries : 1];
+  __shared__ int64_t lds_end[kLds ? 64 : 1];
+  const int nb = (int)mask + 1;
   const int64_t* off = place_off;
   const int64_t* ends = rend;
   if (kLds) {
-    for (int i = threadIdx.x; i < P * kBuckets; i += kPlaceBlock) lds_off[i] = place_off[i];
+    for (int i = threadIdx.x; i < P * nb; i += kPlaceBlock) lds_off[i] = place_off[i];
     for (int i = threadIdx.x; i < P; i += kPlaceBlock) lds_end[i] = rend[i];
     __syncthreads();
     off = lds_off;
@@ -413,14 +444,76 @@ __global__ __launch_bounds__(kPlaceBlock) void k_place(const Elem* __restrict__ 
     const Elem x = load_elem(recv + k);
     int s = 0;
     while (s < P - 1 && k >= ends[s]) ++s;  // first source whose segment holds k
-    const uint32_t d = (uint32_t)(x.key >> shift) & (kBuckets - 1);
-    store_elem(A + (off[s * kBuckets + d] + k), x);
+    const uint32_t d = (uint32_t)(x.key >> shift) & mask;
+    store_elem(A + (off[(int64_t)s * nb + d] + k), x);
+  }
+}
+
+// --------------------------------------------- 16-bit digit counts (P > 1)
+// After the two 8-bit local sub-passes of a 16-bit digit the rank's records
+// are sorted by that digit, so its 65536-bin histogram is the run lengths:
+// k_digit_starts marks the first index of every present digit, k_starts_to_counts
+// turns starts into counts (an absent digit counts 0).
+__global__ __launch_bounds__(256) void k_digit_starts(const Elem* __restrict__ A, int64_t m,
+                                                      int shift, int64_t* __restrict__ first) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < m; i += stride) {
+    const uint32_t d = (uint32_t)(A[i].key >> shift) & 0xFFFFu;
+    if (i == 0 || ((uint32_t)(A[i - 1].key >> shift) & 0xFFFFu) != d) first[d] = i;
+  }
+}
+
+constexpr int kStartsBlock = 1024;
+constexpr int kStartsPer = 65536 / kStartsBlock;  // 64 digits per thread
+
+// One workgroup.  first[d] = -1 for absent digits.
+__global__ __launch_bounds__(kStartsBlock) void k_starts_to_counts(const int64_t* __restrict__ first,
+                                                                   int64_t m,
+                                                                   uint64_t* __restrict__ counts) {
+  __shared__ int64_t nxt[kStartsBlock / 64];
+  const int t = threadIdx.x;
+  const int d0 = t * kStartsPer;
+  // first present start in my range (or m): the suffix-min seen by the thread before me
+  int64_t mine = m;
+  for (int j = kStartsPer - 1; j >= 0; --j) {
+    const int64_t f = first[d0 + j];
+    if (f >= 0) mine = f;
+  }
+  // suffix min over threads t+1.. (starts increase with the digit, so the
+  // next present start after my range is the first present start of the
+  // nearest later thread that has one)
+  int64_t after = m;
+  {
+    int64_t v = mine;
+    const uint32_t lane = lane_id();
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int64_t u = __shfl_down(v, off, 64);
+      if (lane + off < 64) v = u < v ? u : v;
+    }
+    // v = min over lanes >= lane in this wave; need strictly later threads
+    const int64_t later_in_wave = __shfl_down(v, 1, 64);
+    if (lane == 0) nxt[t >> 6] = v;
+    __syncthreads();
+    int64_t later_waves = m;
+    for (int w = (t >> 6) + 1; w < kStartsBlock / 64; ++w) later_waves = nxt[w] < later_waves ? nxt[w] : later_waves;
+    after = lane == 63 ? later_waves : (later_in_wave < later_waves ? later_in_wave : later_waves);
+  }
+  int64_t next = after;
+  for (int j = kStartsPer - 1; j >= 0; --j) {
+    const int64_t f = first[d0 + j];
+    if (f >= 0) {
+      counts[d0 + j] = (uint64_t)(next - f);
+      next = f;
+    } else {
+      counts[d0 + j] = 0;
+    }
   }
 }
 
 // ------------------------------------------------------------------ checks
 __global__ __launch_bounds__(256) void k_verify(const Elem* __restrict__ A, int64_t here,
-                                                int64_t gbase, int64_t n, int64_t per,
+                                                int64_t gbase, int64_t n, int64_t per, KeyGen gen,
                                                 unsigned long long* first_bad) {
   const int64_t stride = (int64_t)gridDim.x * 256;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < here; i += stride) {
@@ -429,7 +522,7 @@ __global__ __launch_bounds__(256) void k_verify(const Elem* __restrict__ A, int6
     if (!bad) {
       const uint64_t r = x.val / (uint64_t)per;
       const uint64_t idx = x.val - r * (uint64_t)per;
-      bad = pcg_output(pcg_jump(pcg_seed(r), idx + 1)) != x.key;
+      bad = make_key(pcg_output(pcg_jump(pcg_seed(r), idx + 1)), gen) != x.key;
     }
     if (i + 1 < here) {
       const Elem y = load_elem(A + i + 1);
@@ -466,11 +559,24 @@ Chunking make_chunking(int64_t m, int max_chunks) {
   return ch;
 }
 
-hipError_t launch_pcg_fill(Elem* A, int64_t count, uint64_t seed, uint64_t val0, hipStream_t s) {
+hipError_t launch_pcg_fill(Elem* A, int64_t count, uint64_t seed, uint64_t val0, KeyGen gen,
+                           hipStream_t s) {
   if (count <= 0) return hipSuccess;
   const int64_t threads = (count + kFillPerThread - 1) / kFillPerThread;
   const int64_t blocks = (threads + 255) / 256;
-  hipLaunchKernelGGL(k_pcg_fill, dim3((unsigned)blocks), dim3(256), 0, s, A, count, seed, val0);
+  hipLaunchKernelGGL(k_pcg_fill, dim3((unsigned)blocks), dim3(256), 0, s, A, count, seed, val0,
+                     gen);
+  return hipGetLastError();
+}
+
+hipError_t launch_digit16_counts(const Elem* A, int64_t m, int shift, int64_t* first,
+                                 uint64_t* counts, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(first, 0xff, sizeof(int64_t) * 65536, s);
+  if (e != hipSuccess) return e;
+  if (m > 0)
+    hipLaunchKernelGGL(k_digit_starts, dim3(grid_for(m, 256, 8192)), dim3(256), 0, s, A, m, shift,
+                       first);
+  hipLaunchKernelGGL(k_starts_to_counts, dim3(1), dim3(kStartsBlock), 0, s, first, m, counts);
   return hipGetLastError();
 }
 
@@ -500,25 +606,26 @@ hipError_t launch_scatter(const Elem* in, Elem* out, int64_t m, int shift, Chunk
   return hipGetLastError();
 }
 
-hipError_t launch_place(const Elem* recv, Elem* A, int64_t m, int shift, int P, const int64_t* rend,
-                        const int64_t* place_off, hipStream_t s) {
+hipError_t launch_place(const Elem* recv, Elem* A, int64_t m, int shift, int nbuckets, int P,
+                        const int64_t* rend, const int64_t* place_off, hipStream_t s) {
   if (m <= 0) return hipSuccess;
-  if (P < 1) return hipErrorInvalidValue;
+  if (P < 1 || P > 64 || (nbuckets != 256 && nbuckets != 65536)) return hipErrorInvalidValue;
   const dim3 grid(grid_for(m, kPlaceBlock, 4096));
-  if (P <= kPlaceLdsRanks)
-    hipLaunchKernelGGL(k_place<true>, grid, dim3(kPlaceBlock), 0, s, recv, A, m, shift, P, rend,
-                       place_off);
+  const uint32_t mask = (uint32_t)nbuckets - 1;
+  if ((int64_t)P * nbuckets <= kPlaceLdsEntries)
+    hipLaunchKernelGGL(k_place<true>, grid, dim3(kPlaceBlock), 0, s, recv, A, m, shift, mask, P,
+                       rend, place_off);
   else
-    hipLaunchKernelGGL(k_place<false>, grid, dim3(kPlaceBlock), 0, s, recv, A, m, shift, P, rend,
-                       place_off);
+    hipLaunchKernelGGL(k_place<false>, grid, dim3(kPlaceBlock), 0, s, recv, A, m, shift, mask, P,
+                       rend, place_off);
   return hipGetLastError();
 }
 
 hipError_t launch_verify(const Elem* A, int64_t here, int64_t gbase, int64_t n, int64_t per,
-                         unsigned long long* first_bad, hipStream_t s) {
+                         KeyGen gen, unsigned long long* first_bad, hipStream_t s) {
   if (here <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_verify, dim3(grid_for(here, 256, 8192)), dim3(256), 0, s, A, here, gbase, n,
-                     per, first_bad);
+                     per, gen, first_bad);
   return hipGetLastError();
 }
 

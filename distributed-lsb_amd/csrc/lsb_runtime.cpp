@@ -1,21 +1,24 @@
 // Runtime behind include/lsb.h: contexts, device buffers, the pass loop
 // (mySort / globalShuffle) and the exchange (RCCL or in-process loopback).
 //
-// Per pass on digit d (64 / 8 passes, least significant first,
-// mpi/mpi_lsbsort.cpp:580-585), for every rank r:
-//   1. local stable pass A -> B on digit d            k_upsweep, k_scan, k_scatter
-//      (localShuffle, mpi/mpi_lsbsort.cpp:213-247).  B is then bucket-ordered.
-//   P == 1: B is the answer for this digit; A and B swap.
+// Per pass on digit d of `bits` bits (64 / bits passes, least significant
+// first, mpi/mpi_lsbsort.cpp:580-585), for every rank r:
+//   1. local stable pass(es) A -> B, then swap (localShuffle,
+//      mpi/mpi_lsbsort.cpp:213-247): one 8-bit pass for bits = 8, two stable
+//      8-bit sub-passes (low byte, high byte) for bits = 16.  A is then
+//      ordered by digit d.
+//   P == 1: done.
 //   P  > 1:
-//   2. all-gather of the 256 bucket counts of every rank
-//      (replaces copyCountsToGlobalCounts + MPI_Exscan + copyStartsFromGlobalStarts,
-//       mpi/mpi_lsbsort.cpp:327-479: every rank then scans the P x 256 matrix
-//       in digit-major, rank-minor order itself)
-//   3. host plan: per-peer send/recv counts and the placement table
-//   4. all-to-all-v of the 16-byte records (MPI_Alltoallv of 24-byte
-//      ShuffleBufSortElement at mpi/mpi_lsbsort.cpp:563; here no dst index
-//      travels: the receiver derives it from the gathered counts)
-//   5. k_place: received runs -> A (mpi/mpi_lsbsort.cpp:568-575)
+//   2. the rank's bucket counts of digit d (k_scan totals for 8 bits,
+//      run lengths of the sorted 16-bit digits for 16 bits), all-gathered
+//      (replaces copyCountsToGlobalCounts + MPI_Exscan +
+//      copyStartsFromGlobalStarts, mpi/mpi_lsbsort.cpp:327-479: every rank
+//      scans the P x nbuckets matrix in digit-major, rank-minor order itself)
+//   3. host plan (lsb_plan_exchange): per-peer send/recv counts, placement table
+//   4. all-to-all-v of 16-byte records out of A into R (MPI_Alltoallv of
+//      24-byte ShuffleBufSortElement at mpi/mpi_lsbsort.cpp:563; no
+//      destination index travels: the receiver derives it from the counts)
+//   5. k_place: R -> B, swap (mpi/mpi_lsbsort.cpp:568-575)
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -48,18 +51,19 @@ struct Rank {
   hipStream_t stream = nullptr;
   int64_t here = 0;
   Elem* A = nullptr;  // per slots: input / output (DistributedArray A)
-  Elem* B = nullptr;  // per slots: scratch; the bucket-ordered send buffer when P > 1
+  Elem* B = nullptr;  // per slots: ping-pong partner
   Elem* R = nullptr;  // per slots: receive buffer (P > 1 only)
-  uint32_t* chunk_hist = nullptr;       // [256][kMaxChunks]
-  uint64_t* chunk_off = nullptr;        // [256][kMaxChunks]
-  uint64_t* totals = nullptr;           // [256]  local bucket counts of the current digit
-  uint64_t* gather = nullptr;           // [P][256] all-gathered counts (RCCL mode)
-  int64_t* place = nullptr;             // [P][256] place_off, then [P] rend
+  uint32_t* chunk_hist = nullptr;       // [256][num_chunks]
+  uint64_t* chunk_off = nullptr;        // [256][num_chunks]
+  uint64_t* totals = nullptr;           // [256] local counts of the current 8-bit digit
+  uint64_t* totals16 = nullptr;         // [65536] local counts of a 16-bit digit (bits = 16, P > 1)
+  int64_t* first16 = nullptr;           // [65536] scratch of the 16-bit count
+  uint64_t* gather = nullptr;           // [P][nb] all-gathered counts
+  int64_t* place = nullptr;             // [P][nb] place_off, then [P] rend
   unsigned long long* check = nullptr;  // [4] verify / check_sorted scratch
   uint64_t* gather_h = nullptr;         // pinned host mirrors
   int64_t* place_h = nullptr;
   lsb::Chunking chunking;
-  int max_chunks = 0;
   std::vector<int64_t> send_counts, send_displs, recv_counts, recv_displs;
 };
 
@@ -70,18 +74,20 @@ struct lsb_ctx {
   int64_t n = 0;
   int64_t per = 0;
   int P = 1;
-  int bits = 8;
+  int bits = 8;      // exchange digit width: 8 or 16
+  int nb = 256;      // 1 << bits
   int first_rank = 0;
   std::vector<Rank> ranks;  // local ranks
   ncclComm_t comm = nullptr;
   bool timing = false;
   bool force_exchange = false;
+  lsb::KeyGen keygen;
   std::vector<PendingEvent> pending;
   std::vector<hipEvent_t> event_pool;
   int64_t launches[LSB_K_COUNT] = {};
   double total_ms[LSB_K_COUNT] = {};
   int64_t scatter_elems = 0;
-  std::vector<int64_t> hist_h;  // [P][256] as int64 for the planner
+  std::vector<int64_t> hist_h;  // [P][nb] as int64 for the planner
 };
 
 namespace {
@@ -195,7 +201,7 @@ int host_alloc(T** p, size_t count) {
 int max_chunks_for_device(int dev) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, dev) != hipSuccess || prop.multiProcessorCount <= 0) return 512;
-  // Two scatter workgroups fit one CU (70 KiB LDS each): one chunk per slot.
+  // Two scatter workgroups fit one CU (72 KiB LDS each): one chunk per slot.
   return std::min(lsb::kMaxChunks, 2 * prop.multiProcessorCount);
 }
 
@@ -206,20 +212,24 @@ int init_rank(lsb_ctx* c, Rank& r, int rank, int dev) {
   HIP_TRY(hipSetDevice(dev));
   HIP_TRY(hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking));
   const size_t per = (size_t)c->per;
+  r.chunking = lsb::make_chunking(r.here, max_chunks_for_device(dev));
+  const size_t hist_entries = (size_t)lsb::kBuckets * std::max(1, r.chunking.num_chunks);
+  const size_t P = (size_t)c->P, nb = (size_t)c->nb;
   LSB_TRY(dev_alloc(&r.A, per));
   LSB_TRY(dev_alloc(&r.B, per));
-  if (exchanging(c) || c->P > 1) LSB_TRY(dev_alloc(&r.R, per));
-  const size_t hist_entries = (size_t)lsb::kBuckets * lsb::kMaxChunks;
+  if (c->P > 1) LSB_TRY(dev_alloc(&r.R, per));
   LSB_TRY(dev_alloc(&r.chunk_hist, hist_entries));
   LSB_TRY(dev_alloc(&r.chunk_off, hist_entries));
   LSB_TRY(dev_alloc(&r.totals, lsb::kBuckets));
-  LSB_TRY(dev_alloc(&r.gather, (size_t)c->P * lsb::kBuckets));
-  LSB_TRY(dev_alloc(&r.place, (size_t)c->P * lsb::kBuckets + c->P));
+  if (c->bits == 16) {
+    LSB_TRY(dev_alloc(&r.totals16, 65536));
+    LSB_TRY(dev_alloc(&r.first16, 65536));
+  }
+  LSB_TRY(dev_alloc(&r.gather, std::max(P * nb, P * 4)));
+  LSB_TRY(dev_alloc(&r.place, P * nb + P));
   LSB_TRY(dev_alloc(&r.check, 4));
-  LSB_TRY(host_alloc(&r.gather_h, (size_t)c->P * lsb::kBuckets));
-  LSB_TRY(host_alloc(&r.place_h, (size_t)c->P * lsb::kBuckets + c->P));
-  r.max_chunks = max_chunks_for_device(dev);
-  r.chunking = lsb::make_chunking(r.here, r.max_chunks);
+  LSB_TRY(host_alloc(&r.gather_h, P * nb));
+  LSB_TRY(host_alloc(&r.place_h, P * nb + P));
   r.send_counts.assign(c->P, 0);
   r.send_displs.assign(c->P, 0);
   r.recv_counts.assign(c->P, 0);
@@ -238,6 +248,8 @@ void free_rank(Rank& r) {
   (void)hipFree(r.chunk_hist);
   (void)hipFree(r.chunk_off);
   (void)hipFree(r.totals);
+  (void)hipFree(r.totals16);
+  (void)hipFree(r.first16);
   (void)hipFree(r.gather);
   (void)hipFree(r.place);
   (void)hipFree(r.check);
@@ -253,14 +265,13 @@ Rank* local_rank(lsb_ctx* c, int rank) {
   return &c->ranks[i];
 }
 
-// ---- one local stable pass A -> B (localShuffle) ------------------------
+// ---- one local stable 8-bit pass A -> B, then swap (localShuffle) -------
 int local_pass(lsb_ctx* c, Rank& r, int shift) {
+  HIP_TRY(hipSetDevice(r.dev));
   if (r.here == 0) {
-    HIP_TRY(hipSetDevice(r.dev));
     HIP_TRY(hipMemsetAsync(r.totals, 0, sizeof(uint64_t) * lsb::kBuckets, r.stream));
     return LSB_OK;
   }
-  HIP_TRY(hipSetDevice(r.dev));
   const lsb::Chunking& ch = r.chunking;
   {
     Timer t(c, &r, LSB_K_UPSWEEP);
@@ -275,58 +286,80 @@ int local_pass(lsb_ctx* c, Rank& r, int shift) {
     HIP_TRY(lsb::launch_scatter(r.A, r.B, r.here, shift, ch, r.chunk_off, r.totals, r.stream));
     if (c->timing) c->scatter_elems += r.here;
   }
+  std::swap(r.A, r.B);
+  return LSB_OK;
+}
+
+// Device counts of the exchange digit for rank r (A is ordered by it).
+int digit_counts(lsb_ctx* c, Rank& r, int digit, const uint64_t** counts) {
+  if (c->bits == 8) {
+    *counts = r.totals;  // k_scan totals of the (only) sub-pass
+    return LSB_OK;
+  }
+  HIP_TRY(hipSetDevice(r.dev));
+  {
+    Timer t(c, &r, LSB_K_UPSWEEP);
+    HIP_TRY(lsb::launch_digit16_counts(r.A, r.here, digit * 16, r.first16, r.totals16, r.stream));
+  }
+  *counts = r.totals16;
   return LSB_OK;
 }
 
 // Turn the host plan of rank r into the device placement table.
 int upload_plan(lsb_ctx* c, Rank& r) {
-  const int P = c->P;
-  int64_t* rend = r.place_h + (size_t)P * lsb::kBuckets;
+  const size_t PN = (size_t)c->P * c->nb;
+  int64_t* rend = r.place_h + PN;
   int64_t acc = 0;
-  for (int s = 0; s < P; ++s) {
+  for (int s = 0; s < c->P; ++s) {
     acc += r.recv_counts[s];
     rend[s] = acc;
   }
   HIP_TRY(hipSetDevice(r.dev));
-  HIP_TRY(hipMemcpyAsync(r.place, r.place_h, sizeof(int64_t) * ((size_t)P * lsb::kBuckets + P),
-                         hipMemcpyHostToDevice, r.stream));
+  HIP_TRY(hipMemcpyAsync(r.place, r.place_h, sizeof(int64_t) * (PN + c->P), hipMemcpyHostToDevice,
+                         r.stream));
   return LSB_OK;
 }
 
 int plan_rank(lsb_ctx* c, Rank& r) {
-  return lsb_plan_exchange(c->n, c->P, r.rank, lsb::kBuckets, c->hist_h.data(), r.send_counts.data(),
+  return lsb_plan_exchange(c->n, c->P, r.rank, c->nb, c->hist_h.data(), r.send_counts.data(),
                            r.send_displs.data(), r.recv_counts.data(), r.recv_displs.data(),
                            r.place_h);
 }
 
+// R -> B by the plan, then swap: A holds the pass result.
 int place_rank(lsb_ctx* c, Rank& r, int shift) {
-  Timer t(c, &r, LSB_K_PLACE);
-  HIP_TRY(hipSetDevice(r.dev));
-  const int64_t* rend = r.place + (size_t)c->P * lsb::kBuckets;
-  HIP_TRY(lsb::launch_place(r.R, r.A, r.here, shift, c->P, rend, r.place, r.stream));
+  {
+    Timer t(c, &r, LSB_K_PLACE);
+    HIP_TRY(hipSetDevice(r.dev));
+    const int64_t* rend = r.place + (size_t)c->P * c->nb;
+    HIP_TRY(lsb::launch_place(r.R, r.B, r.here, shift, c->nb, c->P, rend, r.place, r.stream));
+  }
+  std::swap(r.A, r.B);
   return LSB_OK;
 }
 
 // ---- exchange: in-process loopback --------------------------------------
-int exchange_loopback(lsb_ctx* c, int shift) {
+int exchange_loopback(lsb_ctx* c, int digit) {
+  const int shift = digit * c->bits;
+  const size_t nb = (size_t)c->nb;
   // counts of every rank -> host (stands in for ncclAllGather)
   for (Rank& r : c->ranks) {
-    HIP_TRY(hipSetDevice(r.dev));
-    HIP_TRY(hipMemcpyAsync(r.gather_h, r.totals, sizeof(uint64_t) * lsb::kBuckets,
-                           hipMemcpyDeviceToHost, r.stream));
+    const uint64_t* counts = nullptr;
+    LSB_TRY(digit_counts(c, r, digit, &counts));
+    HIP_TRY(hipMemcpyAsync(r.gather_h, counts, sizeof(uint64_t) * nb, hipMemcpyDeviceToHost,
+                           r.stream));
   }
   for (Rank& r : c->ranks) {
     HIP_TRY(hipSetDevice(r.dev));
     HIP_TRY(hipStreamSynchronize(r.stream));
   }
   for (Rank& r : c->ranks)
-    for (int b = 0; b < lsb::kBuckets; ++b)
-      c->hist_h[(size_t)r.rank * lsb::kBuckets + b] = (int64_t)r.gather_h[b];
+    for (size_t b = 0; b < nb; ++b) c->hist_h[(size_t)r.rank * nb + b] = (int64_t)r.gather_h[b];
   for (Rank& r : c->ranks) {
     LSB_TRY(plan_rank(c, r));
     LSB_TRY(upload_plan(c, r));
   }
-  // all-to-all-v: segment q of rank s's bucket-ordered B -> rank q's R.
+  // all-to-all-v: segment q of rank s's digit-ordered A -> rank q's R.
   for (Rank& q : c->ranks) {
     Timer t(c, &q, LSB_K_EXCHANGE);
     HIP_TRY(hipSetDevice(q.dev));
@@ -335,32 +368,37 @@ int exchange_loopback(lsb_ctx* c, int shift) {
       if (cnt != q.recv_counts[s.rank])
         return fail(LSB_ERR_STATE, "exchange_loopback", "send/recv count mismatch");
       if (cnt == 0) continue;
-      HIP_TRY(hipMemcpyAsync(q.R + q.recv_displs[s.rank], s.B + s.send_displs[q.rank],
+      HIP_TRY(hipMemcpyAsync(q.R + q.recv_displs[s.rank], s.A + s.send_displs[q.rank],
                              (size_t)cnt * sizeof(Elem), hipMemcpyDefault, q.stream));
     }
   }
-  for (Rank& r : c->ranks) LSB_TRY(place_rank(c, r, shift));
-  // The next pass rewrites every B that these copies read, on other streams.
+  // Every rank's copies must be done before any rank's placement reuses B/A
+  // (placement writes B, the next pass rewrites the A that was copied from).
   for (Rank& r : c->ranks) {
     HIP_TRY(hipSetDevice(r.dev));
     HIP_TRY(hipStreamSynchronize(r.stream));
   }
+  for (Rank& r : c->ranks) LSB_TRY(place_rank(c, r, shift));
   return LSB_OK;
 }
 
 // ---- exchange: RCCL (one rank per process) ------------------------------
-int exchange_rccl(lsb_ctx* c, int shift) {
+int exchange_rccl(lsb_ctx* c, int digit) {
+  const int shift = digit * c->bits;
   const int P = c->P;
+  const size_t nb = (size_t)c->nb;
   Rank& r = c->ranks[0];
+  const uint64_t* counts = nullptr;
+  LSB_TRY(digit_counts(c, r, digit, &counts));
   HIP_TRY(hipSetDevice(r.dev));
   {
     Timer t(c, &r, LSB_K_EXCHANGE);
-    RCCL_TRY(ncclAllGather(r.totals, r.gather, lsb::kBuckets, ncclUint64, c->comm, r.stream));
+    RCCL_TRY(ncclAllGather(counts, r.gather, nb, ncclUint64, c->comm, r.stream));
   }
-  HIP_TRY(hipMemcpyAsync(r.gather_h, r.gather, sizeof(uint64_t) * (size_t)P * lsb::kBuckets,
+  HIP_TRY(hipMemcpyAsync(r.gather_h, r.gather, sizeof(uint64_t) * (size_t)P * nb,
                          hipMemcpyDeviceToHost, r.stream));
   HIP_TRY(hipStreamSynchronize(r.stream));
-  for (size_t i = 0; i < (size_t)P * lsb::kBuckets; ++i) c->hist_h[i] = (int64_t)r.gather_h[i];
+  for (size_t i = 0; i < (size_t)P * nb; ++i) c->hist_h[i] = (int64_t)r.gather_h[i];
   LSB_TRY(plan_rank(c, r));
   LSB_TRY(upload_plan(c, r));
   {
@@ -370,14 +408,14 @@ int exchange_rccl(lsb_ctx* c, int shift) {
     if (r.send_counts[me] != r.recv_counts[me])
       return fail(LSB_ERR_STATE, "exchange_rccl", "self count mismatch");
     if (r.send_counts[me] > 0)
-      HIP_TRY(hipMemcpyAsync(r.R + r.recv_displs[me], r.B + r.send_displs[me],
+      HIP_TRY(hipMemcpyAsync(r.R + r.recv_displs[me], r.A + r.send_displs[me],
                              (size_t)r.send_counts[me] * sizeof(Elem), hipMemcpyDeviceToDevice,
                              r.stream));
     RCCL_TRY(ncclGroupStart());
     for (int q = 0; q < P; ++q) {
       if (q == me) continue;
       if (r.send_counts[q] > 0)
-        RCCL_TRY(ncclSend(r.B + r.send_displs[q], (size_t)r.send_counts[q] * 2, ncclUint64, q,
+        RCCL_TRY(ncclSend(r.A + r.send_displs[q], (size_t)r.send_counts[q] * 2, ncclUint64, q,
                           c->comm, r.stream));
       if (r.recv_counts[q] > 0)
         RCCL_TRY(ncclRecv(r.R + r.recv_displs[q], (size_t)r.recv_counts[q] * 2, ncclUint64, q,
@@ -389,14 +427,11 @@ int exchange_rccl(lsb_ctx* c, int shift) {
 }
 
 int do_pass(lsb_ctx* c, int digit) {
-  const int shift = digit * lsb::kDigitBits;
-  for (Rank& r : c->ranks) LSB_TRY(local_pass(c, r, shift));
-  if (!exchanging(c)) {
-    for (Rank& r : c->ranks) std::swap(r.A, r.B);
-    return LSB_OK;
-  }
-  if (c->mode == Mode::kRccl) return exchange_rccl(c, shift);
-  return exchange_loopback(c, shift);
+  for (int sub = 0; sub < c->bits / lsb::kDigitBits; ++sub)
+    for (Rank& r : c->ranks) LSB_TRY(local_pass(c, r, digit * c->bits + sub * lsb::kDigitBits));
+  if (!exchanging(c)) return LSB_OK;
+  if (c->mode == Mode::kRccl) return exchange_rccl(c, digit);
+  return exchange_loopback(c, digit);
 }
 
 int check_ctx(const lsb_ctx* c) {
@@ -404,9 +439,16 @@ int check_ctx(const lsb_ctx* c) {
   return LSB_OK;
 }
 
-int finish_create(lsb_ctx* c, lsb_ctx_t** out) {
-  *out = c;
-  return LSB_OK;
+lsb_ctx* new_ctx(int64_t n_total, int num_ranks, int radix_bits) {
+  lsb_ctx* c = new (std::nothrow) lsb_ctx();
+  if (!c) return nullptr;
+  c->n = n_total;
+  c->P = num_ranks;
+  c->per = div_ceil(n_total, num_ranks);
+  c->bits = radix_bits;
+  c->nb = 1 << radix_bits;
+  c->hist_h.assign((size_t)num_ranks * c->nb, 0);
+  return c;
 }
 
 // Boundary records of every rank (first, last of its here-part), gathered on
@@ -418,6 +460,7 @@ int gather_boundaries(lsb_ctx* c, std::vector<uint64_t>& bnd) {
     for (Rank& r : c->ranks) {
       if (r.here == 0) continue;
       HIP_TRY(hipSetDevice(r.dev));
+      HIP_TRY(hipStreamSynchronize(r.stream));
       HIP_TRY(hipMemcpy(&bnd[(size_t)r.rank * 4], r.A, 16, hipMemcpyDeviceToHost));
       HIP_TRY(hipMemcpy(&bnd[(size_t)r.rank * 4 + 2], r.A + (r.here - 1), 16, hipMemcpyDeviceToHost));
     }
@@ -425,14 +468,14 @@ int gather_boundaries(lsb_ctx* c, std::vector<uint64_t>& bnd) {
   }
   Rank& r = c->ranks[0];
   HIP_TRY(hipSetDevice(r.dev));
-  uint64_t* d = r.gather;  // reuse: needs 4*P <= 256*P entries
+  uint64_t* d = r.gather;  // >= 4 * P entries
   HIP_TRY(hipMemsetAsync(d, 0, sizeof(uint64_t) * 4 * P, r.stream));
   if (r.here > 0) {
     HIP_TRY(hipMemcpyAsync(d + (size_t)r.rank * 4, r.A, 16, hipMemcpyDeviceToDevice, r.stream));
     HIP_TRY(hipMemcpyAsync(d + (size_t)r.rank * 4 + 2, r.A + (r.here - 1), 16,
                            hipMemcpyDeviceToDevice, r.stream));
   }
-  // Each rank contributes its own 4 words (in place all-gather).
+  // Each rank contributes its own 4 words (in-place all-gather).
   RCCL_TRY(ncclAllGather(d + (size_t)r.rank * 4, d, 4, ncclUint64, c->comm, r.stream));
   HIP_TRY(hipMemcpyAsync(bnd.data(), d, sizeof(uint64_t) * 4 * P, hipMemcpyDeviceToHost, r.stream));
   HIP_TRY(hipStreamSynchronize(r.stream));
@@ -483,17 +526,14 @@ int lsb_create(lsb_ctx_t** out, int64_t n_total, int num_ranks, const int* dev_i
                int radix_bits) {
   if (!out) return fail(LSB_ERR_INVALID, "lsb_create", "null out");
   *out = nullptr;
-  if (n_total < 0 || num_ranks < 1) return fail(LSB_ERR_INVALID, "lsb_create", "n or P");
-  if (radix_bits != 8) return fail(LSB_ERR_UNSUPPORTED, "lsb_create", "radix_bits must be 8");
-  lsb_ctx* c = new (std::nothrow) lsb_ctx();
+  if (n_total < 0 || num_ranks < 1 || num_ranks > 64)
+    return fail(LSB_ERR_INVALID, "lsb_create", "n or P");
+  if (radix_bits != 8 && radix_bits != 16)
+    return fail(LSB_ERR_UNSUPPORTED, "lsb_create", "radix_bits must be 8 or 16");
+  lsb_ctx* c = new_ctx(n_total, num_ranks, radix_bits);
   if (!c) return LSB_ERR_NOMEM;
   c->mode = Mode::kLoopback;
-  c->n = n_total;
-  c->P = num_ranks;
-  c->per = div_ceil(n_total, num_ranks);
-  c->bits = radix_bits;
   c->first_rank = 0;
-  c->hist_h.assign((size_t)num_ranks * lsb::kBuckets, 0);
   c->ranks.resize(num_ranks);
   for (int r = 0; r < num_ranks; ++r) {
     int rc = init_rank(c, c->ranks[r], r, dev_ids ? dev_ids[r] : 0);
@@ -502,7 +542,8 @@ int lsb_create(lsb_ctx_t** out, int64_t n_total, int num_ranks, const int* dev_i
       return rc;
     }
   }
-  return finish_create(c, out);
+  *out = c;
+  return LSB_OK;
 }
 
 int lsb_get_unique_id(unsigned char id[LSB_UNIQUE_ID_BYTES]) {
@@ -518,18 +559,14 @@ int lsb_create_rank(lsb_ctx_t** out, int64_t n_total, int num_ranks, int rank, i
                     int radix_bits, const unsigned char id[LSB_UNIQUE_ID_BYTES]) {
   if (!out) return fail(LSB_ERR_INVALID, "lsb_create_rank", "null out");
   *out = nullptr;
-  if (n_total < 0 || num_ranks < 1 || rank < 0 || rank >= num_ranks || !id)
+  if (n_total < 0 || num_ranks < 1 || num_ranks > 64 || rank < 0 || rank >= num_ranks || !id)
     return fail(LSB_ERR_INVALID, "lsb_create_rank", "n, P, rank or id");
-  if (radix_bits != 8) return fail(LSB_ERR_UNSUPPORTED, "lsb_create_rank", "radix_bits must be 8");
-  lsb_ctx* c = new (std::nothrow) lsb_ctx();
+  if (radix_bits != 8 && radix_bits != 16)
+    return fail(LSB_ERR_UNSUPPORTED, "lsb_create_rank", "radix_bits must be 8 or 16");
+  lsb_ctx* c = new_ctx(n_total, num_ranks, radix_bits);
   if (!c) return LSB_ERR_NOMEM;
   c->mode = Mode::kRccl;
-  c->n = n_total;
-  c->P = num_ranks;
-  c->per = div_ceil(n_total, num_ranks);
-  c->bits = radix_bits;
   c->first_rank = rank;
-  c->hist_h.assign((size_t)num_ranks * lsb::kBuckets, 0);
   c->ranks.resize(1);
   int rc = init_rank(c, c->ranks[0], rank, dev_id);
   if (rc == LSB_OK) {
@@ -548,7 +585,8 @@ int lsb_create_rank(lsb_ctx_t** out, int64_t n_total, int num_ranks, int rank, i
     lsb_destroy(c);
     return rc;
   }
-  return finish_create(c, out);
+  *out = c;
+  return LSB_OK;
 }
 
 void lsb_destroy(lsb_ctx_t* c) {
@@ -567,7 +605,7 @@ int lsb_set_option(lsb_ctx_t* c, int option, int64_t value) {
       c->timing = value != 0;
       return LSB_OK;
     case LSB_OPT_FORCE_EXCHANGE:
-      if (value && c->P == 1) {
+      if (value) {
         for (Rank& r : c->ranks)
           if (!r.R) {
             HIP_TRY(hipSetDevice(r.dev));
@@ -588,16 +626,30 @@ int lsb_local_ranks(const lsb_ctx_t* c, int* first_rank, int* num_local) {
   return LSB_OK;
 }
 
-int lsb_generate(lsb_ctx_t* c) {
+int lsb_generate_ex(lsb_ctx_t* c, int dist, double param) {
   LSB_TRY(check_ctx(c));
+  lsb::KeyGen g;
+  if (dist == LSB_DIST_UNIFORM) {
+    g.dist = lsb::kDistUniform;
+  } else if (dist == LSB_DIST_ZIPF) {
+    if (!(param > 0.0) || param > 16.0) return fail(LSB_ERR_INVALID, "lsb_generate_ex", "zipf s");
+    g.dist = lsb::kDistZipf;
+    g.zipf_s = param;
+    g.zipf_n = 1ull << 30;
+  } else {
+    return fail(LSB_ERR_INVALID, "lsb_generate_ex", "dist");
+  }
+  c->keygen = g;
   for (Rank& r : c->ranks) {
     HIP_TRY(hipSetDevice(r.dev));
     // Every one of the `per` slots, like mpi/mpi_lsbsort.cpp:650-656.
-    HIP_TRY(lsb::launch_pcg_fill(r.A, c->per, (uint64_t)r.rank, (uint64_t)r.rank * c->per,
+    HIP_TRY(lsb::launch_pcg_fill(r.A, c->per, (uint64_t)r.rank, (uint64_t)r.rank * c->per, g,
                                  r.stream));
   }
   return lsb_sync(c);
 }
+
+int lsb_generate(lsb_ctx_t* c) { return lsb_generate_ex(c, LSB_DIST_UNIFORM, 0.0); }
 
 int lsb_copy_in(lsb_ctx_t* c, int rank, int64_t off, int64_t cnt, const lsb_elem_t* host) {
   LSB_TRY(check_ctx(c));
@@ -665,8 +717,8 @@ int lsb_verify(lsb_ctx_t* c, int64_t* first_bad) {
   for (Rank& r : c->ranks) {
     HIP_TRY(hipSetDevice(r.dev));
     HIP_TRY(hipMemsetAsync(r.check, 0xff, sizeof(unsigned long long), r.stream));
-    HIP_TRY(lsb::launch_verify(r.A, r.here, (int64_t)r.rank * c->per, c->n, c->per, r.check,
-                               r.stream));
+    HIP_TRY(lsb::launch_verify(r.A, r.here, (int64_t)r.rank * c->per, c->n, c->per, c->keygen,
+                               r.check, r.stream));
     unsigned long long h = ~0ull;
     HIP_TRY(hipMemcpyAsync(&h, r.check, sizeof h, hipMemcpyDeviceToHost, r.stream));
     HIP_TRY(hipStreamSynchronize(r.stream));
@@ -695,7 +747,6 @@ int lsb_verify(lsb_ctx_t* c, int64_t* first_bad) {
 
 int lsb_check_sorted(lsb_ctx_t* c, int* sorted) {
   LSB_TRY(check_ctx(c));
-  int64_t bad = 0;  // 0 = sorted so far; reduced with min over "sorted" flags
   int local_ok = 1;
   for (Rank& r : c->ranks) {
     HIP_TRY(hipSetDevice(r.dev));
@@ -716,9 +767,9 @@ int lsb_check_sorted(lsb_ctx_t* c, int* sorted) {
     if (prev >= 0 && bnd[(size_t)s * 4 + 0] < bnd[(size_t)prev * 4 + 2]) bounds_ok = 0;
     prev = s;
   }
-  bad = (local_ok && bounds_ok) ? 1 : 0;
-  LSB_TRY(allreduce_min_i64(c, &bad));
-  if (sorted) *sorted = (int)bad;
+  int64_t ok = (local_ok && bounds_ok) ? 1 : 0;  // min-reduced over ranks
+  LSB_TRY(allreduce_min_i64(c, &ok));
+  if (sorted) *sorted = (int)ok;
   return LSB_OK;
 }
 
@@ -763,25 +814,23 @@ int lsb_plan_exchange(int64_t n_total, int P, int me, int nb, const int64_t* his
   for (int q = 0; q < P; ++q) send_counts[q] = recv_counts[q] = 0;
   const int64_t lo_me = (int64_t)me * per;
   const int64_t hi_me = lo_me + here_of(n_total, P, me);
-  // Two sweeps over buckets in global order; base = start of bucket b.
-  int64_t base = 0;
-  // Receive side is built in (s, b) order but the stream from s is ordered
-  // by b, so first collect per-source run pieces, then lay them out.
+  // The stream from source s is ordered by bucket: collect each (s, b)
+  // piece that lands in my range first, then lay the pieces out.
   std::vector<int64_t> piece_lo((size_t)P * nb, 0), piece_len((size_t)P * nb, 0);
+  int64_t base = 0;  // global start of bucket b
   for (int b = 0; b < nb; ++b) {
     int64_t acc = base;
-    int64_t total_b = 0;
     for (int s = 0; s < P; ++s) {
       const int64_t h = hist[(size_t)s * nb + b];
       if (h < 0) return fail(LSB_ERR_INVALID, "lsb_plan_exchange", "negative count");
       const int64_t g0 = acc, g1 = acc + h;
-      if (s == me && h > 0 && per > 0) {
+      if (g1 > n_total) return fail(LSB_ERR_INVALID, "lsb_plan_exchange", "counts exceed n");
+      if (s == me && h > 0) {
         // split my run [g0, g1) over the owners
         int64_t g = g0;
         while (g < g1) {
           const int64_t q = g / per;
           const int64_t qend = std::min(g1, (q + 1) * per);
-          if (q >= P) return fail(LSB_ERR_INVALID, "lsb_plan_exchange", "counts exceed n");
           send_counts[q] += qend - g;
           g = qend;
         }
@@ -794,11 +843,9 @@ int lsb_plan_exchange(int64_t n_total, int P, int me, int nb, const int64_t* his
         recv_counts[s] += hi - lo;
       }
       acc = g1;
-      total_b += h;
     }
-    base += total_b;
+    base = acc;
   }
-  if (base > n_total) return fail(LSB_ERR_INVALID, "lsb_plan_exchange", "counts exceed n");
   int64_t acc = 0;
   for (int q = 0; q < P; ++q) {
     send_displs[q] = acc;

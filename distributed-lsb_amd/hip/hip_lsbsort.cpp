@@ -14,6 +14,8 @@
 //              (default 0), exchange by device copies; same results as
 //              `mpirun -n P mpi_lsbsort` on one GPU.
 //   --json     also print one machine-readable line.
+//   --radix-bits 8|16   exchange digit width (local passes are always 8-bit)
+//   --dist uniform|zipf [--zipf-s S]   key distribution of the same pcg64 stream
 #include <sys/wait.h>
 #include <unistd.h>
 
@@ -38,6 +40,9 @@ struct Options {
   int ranks = 1;
   int device = 0;
   bool json = false;
+  int radix_bits = 8;
+  int dist = LSB_DIST_UNIFORM;
+  double zipf_s = 1.1;
 };
 
 void flush_output() {
@@ -107,7 +112,7 @@ int run(World& w, const Options& o) {
       printf("Generating random values\n");
       flush_output();
     }
-    CHECK(lsb_generate(w.ctx));
+    CHECK(lsb_generate_ex(w.ctx, o.dist, o.zipf_s));
     CHECK(lsb_barrier(w.ctx));
     auto end = std::chrono::steady_clock::now();
     if (w.root()) {
@@ -188,7 +193,7 @@ int run_rank_process(const Options& o, int rank, int read_fd, const std::vector<
   w.per = lsb_per_rank(o.n, o.gpus);
   w.first = rank;
   w.nlocal = 1;
-  CHECK(lsb_create_rank(&w.ctx, o.n, o.gpus, rank, rank, 8, id));
+  CHECK(lsb_create_rank(&w.ctx, o.n, o.gpus, rank, rank, o.radix_bits, id));
   const int status = run(w, o);
   lsb_destroy(w.ctx);
   return status;
@@ -215,6 +220,14 @@ int main(int argc, char* argv[]) {
     else if (a == "--ranks") o.ranks = std::stoi(next());
     else if (a == "--device") o.device = std::stoi(next());
     else if (a == "--json") o.json = true;
+    else if (a == "--radix-bits") o.radix_bits = std::stoi(next());
+    else if (a == "--zipf-s") o.zipf_s = std::stod(next());
+    else if (a == "--dist") {
+      const std::string d = next();
+      if (d == "zipf") o.dist = LSB_DIST_ZIPF;
+      else if (d == "uniform") o.dist = LSB_DIST_UNIFORM;
+      else { fprintf(stderr, "unknown --dist %s\n", d.c_str()); return 2; }
+    }
   }
   if (!o.verify_set) o.verify = (o.n < 128LL * 1024 * 1024);
   if (o.n < 0 || o.ranks < 1 || o.gpus < 0) {
@@ -269,7 +282,7 @@ int main(int argc, char* argv[]) {
   w.first = 0;
   w.nlocal = o.ranks;
   std::vector<int> devs(o.ranks, o.device);
-  CHECK(lsb_create(&w.ctx, o.n, o.ranks, devs.data(), 8));
+  CHECK(lsb_create(&w.ctx, o.n, o.ranks, devs.data(), o.radix_bits));
   const int status = run(w, o);
   lsb_destroy(w.ctx);
   return status;

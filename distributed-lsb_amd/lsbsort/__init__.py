@@ -40,6 +40,7 @@ UNIQUE_ID_BYTES = 128
 
 LSB_OK = 0
 LSB_ERR_VERIFY = 5
+DIST_UNIFORM, DIST_ZIPF = 0, 1
 K_UPSWEEP, K_SCAN, K_SCATTER, K_EXCHANGE, K_PLACE, K_SORT = range(6)
 KERNEL_NAMES = ("upsweep", "scan", "scatter", "exchange", "place", "sort")
 OPT_TIMING, OPT_FORCE_EXCHANGE = 0, 1
@@ -75,6 +76,7 @@ def _lib() -> ctypes.CDLL:
             "lsb_set_option": (i32, [vp, i32, i64]),
             "lsb_local_ranks": (i32, [vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
             "lsb_generate": (i32, [vp]),
+            "lsb_generate_ex": (i32, [vp, i32, ctypes.c_double]),
             "lsb_copy_in": (i32, [vp, i32, i64, i64, vp]),
             "lsb_copy_out": (i32, [vp, i32, i64, i64, vp]),
             "lsb_sort": (i32, [vp]),
@@ -197,8 +199,14 @@ class World:
     def here(self, r: int) -> int:
         return here(self.n, self.P, r)
 
-    def generate(self) -> None:
-        _check(_lib().lsb_generate(self._h), "lsb_generate")
+    def generate(self, dist: str = "uniform", s: float = 1.1) -> None:
+        """pcg64(rank) input; dist "zipf" maps each draw to a skewed key."""
+        if dist == "uniform":
+            _check(_lib().lsb_generate(self._h), "lsb_generate")
+        elif dist == "zipf":
+            _check(_lib().lsb_generate_ex(self._h, DIST_ZIPF, s), "lsb_generate_ex")
+        else:
+            raise ValueError(dist)
 
     def copy_in(self, rank: int, arr: np.ndarray, off: int = 0) -> None:
         arr = np.ascontiguousarray(arr, dtype=ELEM_DTYPE)

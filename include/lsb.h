@@ -76,7 +76,12 @@ int64_t lsb_here(int64_t n_total, int num_ranks, int rank);      /* clamp(n - r*
 
 /* ---- lifecycle ---------------------------------------------------------- */
 /* One process, `num_ranks` logical ranks; rank r lives on device dev_ids[r]
- * (dev_ids == NULL: every rank on device 0).  radix_bits must be 8. */
+ * (dev_ids == NULL: every rank on device 0).  Up to 64 ranks.
+ * radix_bits is the width of the digit the ranks exchange on: 8 (256
+ * buckets, 8 passes) or 16 (65536 buckets, 4 passes: the reference's own
+ * RADIX, mpi/mpi_lsbsort.cpp:21).  On device every digit is sorted by
+ * stable 8-bit local passes (a 16-bit digit = low byte, then high byte), so
+ * the output is the same for both; 16 halves the all-to-alls when P > 1. */
 int  lsb_create(lsb_ctx_t** ctx, int64_t n_total, int num_ranks,
                 const int* dev_ids, int radix_bits);
 /* RCCL bootstrap: rank 0 calls this and ships the bytes to the other ranks
@@ -96,6 +101,15 @@ int  lsb_local_ranks(const lsb_ctx_t* ctx, int* first_rank, int* num_local);
  * rank r and every one of its `per` slots i: key = i-th output of pcg64(r),
  * val = r*per + i.  Untimed in the reference; untimed here. */
 int  lsb_generate(lsb_ctx_t* ctx);
+/* Same stream, other key distributions (build-defined):
+ *   LSB_DIST_UNIFORM         == lsb_generate
+ *   LSB_DIST_ZIPF, param = s key = mix64(k), k = floor of a power law with
+ *                            exponent s on [1, 2^30], drawn by inverse CDF
+ *                            from the same pcg64(r) draw (heavy duplicates).
+ * lsb_verify() recomputes keys with the distribution last generated. */
+#define LSB_DIST_UNIFORM 0
+#define LSB_DIST_ZIPF    1
+int  lsb_generate_ex(lsb_ctx_t* ctx, int dist, double param);
 /* Host <-> A of a local rank, slots [off, off+cnt) of that rank's per slots. */
 int  lsb_copy_in(lsb_ctx_t* ctx, int rank, int64_t off, int64_t cnt, const lsb_elem_t* host);
 int  lsb_copy_out(lsb_ctx_t* ctx, int rank, int64_t off, int64_t cnt, lsb_elem_t* host);

@@ -147,3 +147,38 @@ def test_simulated_exchange_reproduces_golden(lsb_built, oracle_mod, digests, ro
 def test_simulated_exchange_small(lsb_built, oracle_mod, n, P):
     out = simulate(lsb_built, oracle_mod, n, P)
     assert np.array_equal(out, oracle_mod.mpi_sort(n, P))
+
+
+def simulate16(lsbsort, oracle, n, P):
+    """P > 1 pass loop with 16-bit exchange digits (two 8-bit local sub-passes)."""
+    per = -(-n // P)
+    slots = oracle.generate_slots(n, P)
+    A = [slots[r * per: r * per + lsbsort.here(n, P, r)].copy() for r in range(P)]
+    for d in range(4):
+        hist = np.zeros((P, 65536), np.int64)
+        for r in range(P):
+            x, _ = oracle.local_pass(A[r], 8, 2 * d)
+            x, _ = oracle.local_pass(x, 8, 2 * d + 1)
+            A[r] = x
+            dig = ((x["key"] >> np.uint64(16 * d)) & np.uint64(0xFFFF)).astype(np.int64)
+            hist[r] = np.bincount(dig, minlength=65536)
+        plans = [lsbsort.plan_exchange(n, P, r, hist) for r in range(P)]
+        out = []
+        for q in range(P):
+            R = np.concatenate([A[s][plans[s]["send_displs"][q]:plans[s]["send_displs"][q] + plans[s]["send_counts"][q]]
+                                for s in range(P)])
+            ends = np.cumsum(plans[q]["recv_counts"])
+            src = np.searchsorted(ends, np.arange(R.size), side="right")
+            dig = ((R["key"] >> np.uint64(16 * d)) & np.uint64(0xFFFF)).astype(np.int64)
+            dst = plans[q]["place_off"][src, dig] + np.arange(R.size)
+            o = np.empty_like(R)
+            o[dst] = R
+            out.append(o)
+        A = out
+    return np.concatenate(A)
+
+
+@pytest.mark.parametrize("n,P", [(50_003, 3), (1000, 8)])
+def test_simulated_exchange_radix16(lsb_built, oracle_mod, n, P):
+    out = simulate16(lsb_built, oracle_mod, n, P)
+    assert np.array_equal(out, oracle_mod.mpi_sort(n, P))

@@ -248,3 +248,88 @@ def test_harness_one_gpu_process(lsb_built):
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     assert "Array is sorted" in r.stdout
+
+
+# ------------------------------------------------ 16-bit digits (config C5)
+@pytest.mark.parametrize("row", range(5))
+def test_radix16_golden_digests(lsb_built, oracle_mod, digests, row):
+    """The reference's own radix (RADIX 16): 4 passes, 65536-bucket exchange."""
+    d = digests["rows"][row]
+    with lsb_built.World(d["n"], ranks=d["P"], radix_bits=16) as w:
+        w.generate()
+        w.my_sort()
+        assert oracle_mod.digest(w.gather_global()) == d["output"]
+        assert w.verify() == (True, -1)
+
+
+@pytest.mark.parametrize("name", ["all_equal", "two_keys", "hot_bucket", "zipf", "small_range"])
+@pytest.mark.parametrize("P", [1, 3, 8])
+def test_radix16_distributions(lsb_built, oracle_mod, name, P):
+    rng = np.random.default_rng(hash((name, P, 16)) & 0xFFFF)
+    a = _dist(name, 120_007, rng)
+    w = lsb_built.World(a.size, ranks=P, radix_bits=16)
+    w.scatter_global(a)
+    w.my_sort()
+    assert np.array_equal(w.gather_global(), oracle_mod.stable_sort(a))
+    w.close()
+
+
+def test_radix16_single_pass(lsb_built, oracle_mod):
+    rng = np.random.default_rng(16)
+    n = 70_001
+    a = np.zeros(n, dtype=DT)
+    a["key"] = rng.integers(0, 2**64 - 1, n, dtype=np.uint64)
+    a["val"] = np.arange(n, dtype=np.uint64)
+    with lsb_built.World(n, ranks=1, radix_bits=16) as w:
+        w.copy_in(0, a)
+        cur = a
+        for d in (0, 2):
+            w.global_shuffle(d)
+            cur, _ = oracle_mod.local_pass(cur, 16, d)
+            assert np.array_equal(w.copy_out(0), cur)
+
+
+def test_radix16_forced_exchange_and_rccl(lsb_built, oracle_mod, digests):
+    d = next(r for r in digests["rows"] if r["P"] == 1)
+    with lsb_built.World(d["n"], ranks=1, radix_bits=16) as w:
+        w.set_option(lsb_built.OPT_FORCE_EXCHANGE, 1)
+        w.generate()
+        w.my_sort()
+        assert oracle_mod.digest(w.gather_global()) == d["output"]
+    w = lsb_built.World.rank(d["n"], 1, 0, 0, lsb_built.get_unique_id(), radix_bits=16)
+    try:
+        w.set_option(lsb_built.OPT_FORCE_EXCHANGE, 1)
+        w.generate()
+        w.my_sort()
+        w.barrier()
+        assert oracle_mod.digest(w.copy_out(0)) == d["output"]
+    finally:
+        w.close()
+
+
+# ------------------------------------------------------ Zipf keys (config C4)
+@pytest.mark.parametrize("P,bits", [(1, 8), (4, 8), (4, 16), (8, 16)])
+def test_zipf_input_sorts_bit_exact(lsb_built, oracle_mod, P, bits):
+    n = 1_000_003
+    with lsb_built.World(n, ranks=P, radix_bits=bits) as w:
+        w.generate("zipf", 1.1)
+        inp = w.gather_global()
+        assert np.array_equal(inp["val"], np.arange(n, dtype=np.uint64))
+        # heavily skewed: many duplicates, one dominant key (~9% at s = 1.1)
+        uniq, counts = np.unique(inp["key"], return_counts=True)
+        assert uniq.size < n // 2 and counts.max() > n // 20
+        w.my_sort()
+        assert np.array_equal(w.gather_global(), oracle_mod.stable_sort(inp))
+        assert w.verify() == (True, -1)
+        assert w.check_sorted()
+
+
+def test_zipf_verify_uses_zipf_keys(lsb_built):
+    n = 50_000
+    with lsb_built.World(n, ranks=2) as w:
+        w.generate("zipf", 1.3)
+        w.my_sort()
+        assert w.verify() == (True, -1)
+        w.generate()  # uniform again: verify must recompute uniform keys
+        w.my_sort()
+        assert w.verify() == (True, -1)
