@@ -419,6 +419,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_scatter(const Elem* __restrict__ i
 
 // ------------------------------------------------------------------- place
 constexpr int kPlaceBlock = 256;
+constexpr int kPlaceIpt = 8;
 constexpr int kPlaceLdsEntries = 4096;  // P * nbuckets offsets (32 KiB) staged in LDS up to here
 
 template <bool kLds>
@@ -439,13 +440,27 @@ __global__ __launch_bounds__(kPlaceBlock) void k_place(const Elem* __restrict__ 
     off = lds_off;
     ends = lds_end;
   }
-  const int64_t stride = (int64_t)gridDim.x * kPlaceBlock;
-  for (int64_t k = (int64_t)blockIdx.x * kPlaceBlock + threadIdx.x; k < m; k += stride) {
-    const Elem x = load_elem(recv + k);
-    int s = 0;
-    while (s < P - 1 && k >= ends[s]) ++s;  // first source whose segment holds k
-    const uint32_t d = (uint32_t)(x.key >> shift) & mask;
-    store_elem(A + (off[(int64_t)s * nb + d] + k), x);
+  // kPlaceIpt records in flight per thread (a 1-record grid-stride loop
+  // reached 4.4 TB/s; streaming copies need several loads outstanding).
+  const int64_t step = (int64_t)gridDim.x * kPlaceBlock * kPlaceIpt;
+  for (int64_t base = (int64_t)blockIdx.x * kPlaceBlock * kPlaceIpt + threadIdx.x; base < m;
+       base += step) {
+    Elem x[kPlaceIpt];
+#pragma unroll
+    for (int i = 0; i < kPlaceIpt; ++i) {
+      const int64_t k = base + (int64_t)i * kPlaceBlock;
+      x[i] = k < m ? load_elem(recv + k) : Elem{0ull, 0ull};
+    }
+#pragma unroll
+    for (int i = 0; i < kPlaceIpt; ++i) {
+      const int64_t k = base + (int64_t)i * kPlaceBlock;
+      if (k < m) {
+        int s = 0;
+        while (s < P - 1 && k >= ends[s]) ++s;  // first source whose segment holds k
+        const uint32_t d = (uint32_t)(x[i].key >> shift) & mask;
+        store_elem(A + (off[(int64_t)s * nb + d] + k), x[i]);
+      }
+    }
   }
 }
 
@@ -456,10 +471,23 @@ __global__ __launch_bounds__(kPlaceBlock) void k_place(const Elem* __restrict__ 
 // turns starts into counts (an absent digit counts 0).
 __global__ __launch_bounds__(256) void k_digit_starts(const Elem* __restrict__ A, int64_t m,
                                                       int shift, int64_t* __restrict__ first) {
-  const int64_t stride = (int64_t)gridDim.x * 256;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < m; i += stride) {
-    const uint32_t d = (uint32_t)(A[i].key >> shift) & 0xFFFFu;
-    if (i == 0 || ((uint32_t)(A[i - 1].key >> shift) & 0xFFFFu) != d) first[d] = i;
+  constexpr int IPT = 8;
+  const uint64_t* __restrict__ keys = reinterpret_cast<const uint64_t*>(A);
+  const int64_t step = (int64_t)gridDim.x * 256 * IPT;
+  for (int64_t base = (int64_t)blockIdx.x * 256 * IPT + threadIdx.x; base < m; base += step) {
+    uint64_t k[IPT], kp[IPT];
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) {
+      const int64_t i = base + (int64_t)j * 256;
+      k[j] = i < m ? keys[2 * i] : 0ull;
+      kp[j] = (i > 0 && i < m) ? keys[2 * (i - 1)] : 0ull;  // L1/L2 hit: the neighbour lane's line
+    }
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) {
+      const int64_t i = base + (int64_t)j * 256;
+      const uint32_t d = (uint32_t)(k[j] >> shift) & 0xFFFFu;
+      if (i < m && (i == 0 || ((uint32_t)(kp[j] >> shift) & 0xFFFFu) != d)) first[d] = i;
+    }
   }
 }
 

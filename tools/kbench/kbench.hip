@@ -207,7 +207,9 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&b.hist, sizeof(uint32_t) * kBuckets * kMaxChunks));
   CK(hipMalloc(&b.off, sizeof(uint64_t) * kBuckets * kMaxChunks));
   CK(hipMalloc(&b.tot, sizeof(uint64_t) * kBuckets));
-  CK(launch_pcg_fill(b.in, m, 0, 0, 0));
+  KeyGen gen;
+  if (argc > 3 && atoi(argv[3]) == 1) gen.dist = kDistZipf;
+  CK(launch_pcg_fill(b.in, m, 0, 0, gen, 0));
   CK(hipDeviceSynchronize());
   const int reps = 5;
   const double gb = 32.0 * m / 1e9;

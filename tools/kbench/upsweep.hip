@@ -84,7 +84,7 @@ int main() {
   Elem* A; uint32_t *h0, *h1; uint64_t* sink;
   CK(hipMalloc(&A, m * sizeof(Elem)));
   CK(hipMalloc(&h0, 4 << 20)); CK(hipMalloc(&h1, 4 << 20)); CK(hipMalloc(&sink, 8));
-  CK(launch_pcg_fill(A, m, 0, 0, 0));
+  CK(launch_pcg_fill(A, m, 0, 0, KeyGen{}, 0));
   const double gb = 16.0 * m / 1e9;
   std::vector<uint32_t> a(256 * 4096), b(256 * 4096);
   for (int G : {512, 1024, 2048}) {
