@@ -70,6 +70,14 @@ hipError_t launch_scatter(const Elem* in, Elem* out, int64_t m, int shift, Chunk
 hipError_t launch_place(const Elem* recv, Elem* A, int64_t m, int shift, int nbuckets, int P,
                         const int64_t* rend, const int64_t* place_off, hipStream_t s);
 
+// Exchange plan of rank `me` on device from the all-gathered counts
+// hist[s * nb + b] (same rule as the host planner lsb_plan_exchange):
+// place[s * nb + b] = place_off, place[P * nb + s] = rend (inclusive scan of
+// recv counts), counts[0..P) = send counts, counts[P..2P) = recv counts.
+// work: P * nb int64, total: nb int64 scratch.
+hipError_t launch_plan(const uint64_t* hist, int P, int nb, int me, int64_t n, int64_t* work,
+                       int64_t* total, int64_t* place, int64_t* counts, hipStream_t s);
+
 // O(n) bit-exact stable-sort check of a rank's here-part (see lsb_verify).
 // first_bad must hold UINT64_MAX before the launch; receives min bad global index.
 hipError_t launch_verify(const Elem* A, int64_t here, int64_t gbase, int64_t n, int64_t per,

@@ -539,6 +539,129 @@ __global__ __launch_bounds__(kStartsBlock) void k_starts_to_counts(const int64_t
   }
 }
 
+// ------------------------------------------------------------ device plan
+// The exchange plan of rank `me` from the all-gathered counts hist[s][b]
+// (the same rule as the host planner lsb_plan_exchange):
+//   gstart[b][s] = base[b] + colpre[s][b],  base = excl. scan of column sums,
+//   colpre[s][b] = sum_{s'<s} hist[s'][b]   (digit-major, rank-minor order,
+//   mpi/mpi_lsbsort.cpp:350,378,401)
+// k_plan_cols:   colpre (into work) and column totals
+// k_plan_base:   base = exclusive scan of the totals (one workgroup)
+// k_plan_pieces: the piece of run (s, b) inside my range -> len (into work),
+//                its first dest (into place); my own runs -> send counts
+// k_plan_rows:   per source, exclusive scan of piece lengths over buckets
+// k_plan_finish: place_off[s][b] = (piece start - lo) - (recv_displ[s] + k),
+//                rend[s] = inclusive scan of recv counts
+__global__ __launch_bounds__(256) void k_plan_cols(const uint64_t* __restrict__ hist, int P, int nb,
+                                                   int64_t* __restrict__ work,
+                                                   int64_t* __restrict__ total) {
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= nb) return;
+  int64_t t = 0;
+  for (int s = 0; s < P; ++s) {
+    work[(int64_t)s * nb + b] = t;
+    t += (int64_t)hist[(int64_t)s * nb + b];
+  }
+  total[b] = t;
+}
+
+constexpr int kPlanScanBlock = 1024;
+
+// Exclusive scan of v[0..len) in place by one workgroup, returns the sum.
+// Segments of 4 * kPlanScanBlock entries; thread t owns 4 consecutive
+// entries of a segment, so every load and store is coalesced.
+__device__ int64_t block_scan_inplace(int64_t* v, int len, int64_t* tmp) {
+  constexpr int V = 4;
+  int64_t carry = 0;
+  for (int seg = 0; seg < len; seg += V * kPlanScanBlock) {
+    const int i0 = seg + V * (int)threadIdx.x;
+    int64_t x[V];
+    int64_t s = 0;
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      x[j] = i0 + j < len ? v[i0 + j] : 0;
+      s += x[j];
+    }
+    int64_t tot;
+    int64_t pre = carry + block_exclusive_scan<kPlanScanBlock>(s, tmp, &tot);
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      if (i0 + j < len) v[i0 + j] = pre;
+      pre += x[j];
+    }
+    carry += tot;
+  }
+  return carry;
+}
+
+__global__ __launch_bounds__(kPlanScanBlock) void k_plan_base(int64_t* __restrict__ total, int nb) {
+  __shared__ int64_t tmp[kPlanScanBlock / 64];
+  block_scan_inplace(total, nb, tmp);  // total -> base
+}
+
+__global__ __launch_bounds__(256) void k_plan_pieces(const uint64_t* __restrict__ hist, int P, int nb,
+                                                     int me, int64_t per, int64_t lo, int64_t hi,
+                                                     const int64_t* __restrict__ base,
+                                                     int64_t* __restrict__ work,
+                                                     int64_t* __restrict__ place,
+                                                     unsigned long long* __restrict__ send_counts) {
+  // Send counts are summed per workgroup in LDS first: every bucket of a
+  // rank adds to the same few owners, and 65536 same-address global
+  // atomics took 0.8 ms.
+  __shared__ unsigned long long sc[64];
+  if (threadIdx.x < 64) sc[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < (int64_t)P * nb) {
+    const int s = (int)(i / nb);
+    const int b = (int)(i - (int64_t)s * nb);
+    const int64_t h = (int64_t)hist[i];
+    const int64_t g0 = base[b] + work[i];
+    const int64_t g1 = g0 + h;
+    const int64_t plo = g0 > lo ? g0 : lo;
+    const int64_t phi = g1 < hi ? g1 : hi;
+    work[i] = phi > plo ? phi - plo : 0;  // piece length
+    place[i] = plo;                       // piece's first dest (if any)
+    if (s == me && h > 0) {
+      int64_t g = g0;
+      while (g < g1) {  // split my run over its owners
+        const int64_t q = g / per;
+        const int64_t qend = g1 < (q + 1) * per ? g1 : (q + 1) * per;
+        atomicAdd(&sc[q], (unsigned long long)(qend - g));
+        g = qend;
+      }
+    }
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < P && sc[threadIdx.x])
+    atomicAdd(&send_counts[threadIdx.x], sc[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(kPlanScanBlock) void k_plan_rows(int64_t* __restrict__ work, int nb,
+                                                              int64_t* __restrict__ recv_counts) {
+  __shared__ int64_t tmp[kPlanScanBlock / 64];
+  const int s = blockIdx.x;
+  const int64_t tot = block_scan_inplace(work + (int64_t)s * nb, nb, tmp);
+  if (threadIdx.x == 0) recv_counts[s] = tot;
+}
+
+__global__ __launch_bounds__(256) void k_plan_finish(int P, int nb, int64_t lo,
+                                                     const int64_t* __restrict__ work,
+                                                     const int64_t* __restrict__ recv_counts,
+                                                     int64_t* __restrict__ place) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < P) {  // rend
+    int64_t acc = 0;
+    for (int s = 0; s <= (int)i; ++s) acc += recv_counts[s];
+    place[(int64_t)P * nb + i] = acc;
+  }
+  if (i >= (int64_t)P * nb) return;
+  const int s = (int)(i / nb);
+  int64_t displ = 0;
+  for (int q = 0; q < s; ++q) displ += recv_counts[q];
+  place[i] = (place[i] - lo) - (displ + work[i]);
+}
+
 // ------------------------------------------------------------------ checks
 __global__ __launch_bounds__(256) void k_verify(const Elem* __restrict__ A, int64_t here,
                                                 int64_t gbase, int64_t n, int64_t per, KeyGen gen,
@@ -646,6 +769,29 @@ hipError_t launch_place(const Elem* recv, Elem* A, int64_t m, int shift, int nbu
   else
     hipLaunchKernelGGL(k_place<false>, grid, dim3(kPlaceBlock), 0, s, recv, A, m, shift, mask, P,
                        rend, place_off);
+  return hipGetLastError();
+}
+
+hipError_t launch_plan(const uint64_t* hist, int P, int nb, int me, int64_t n, int64_t* work,
+                       int64_t* total, int64_t* place, int64_t* counts, hipStream_t s) {
+  if (P < 1 || me < 0 || me >= P || nb < 1 || n < 0) return hipErrorInvalidValue;
+  const int64_t per = (n + P - 1) / P;
+  const int64_t lo = (int64_t)me * per;
+  int64_t here = n - lo;
+  if (here > per) here = per;
+  if (here < 0) here = 0;
+  const int64_t hi = lo + here;
+  hipError_t e = hipMemsetAsync(counts, 0, sizeof(int64_t) * 2 * P, s);
+  if (e != hipSuccess) return e;
+  const int64_t cells = (int64_t)P * nb;
+  hipLaunchKernelGGL(k_plan_cols, dim3((nb + 255) / 256), dim3(256), 0, s, hist, P, nb, work, total);
+  hipLaunchKernelGGL(k_plan_base, dim3(1), dim3(kPlanScanBlock), 0, s, total, nb);
+  hipLaunchKernelGGL(k_plan_pieces, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, s, hist, P,
+                     nb, me, per, lo, hi, total, work, place,
+                     reinterpret_cast<unsigned long long*>(counts));
+  hipLaunchKernelGGL(k_plan_rows, dim3(P), dim3(kPlanScanBlock), 0, s, work, nb, counts + P);
+  hipLaunchKernelGGL(k_plan_finish, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, s, P, nb,
+                     lo, work, counts + P, place);
   return hipGetLastError();
 }
 

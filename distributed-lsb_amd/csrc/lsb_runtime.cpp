@@ -59,10 +59,12 @@ struct Rank {
   uint64_t* totals16 = nullptr;         // [65536] local counts of a 16-bit digit (bits = 16, P > 1)
   int64_t* first16 = nullptr;           // [65536] scratch of the 16-bit count
   uint64_t* gather = nullptr;           // [P][nb] all-gathered counts
-  int64_t* place = nullptr;             // [P][nb] place_off, then [P] rend
+  int64_t* place = nullptr;             // [P][nb] place_off, then [P] rend (device plan)
+  int64_t* plan_work = nullptr;         // [P][nb] device-plan scratch
+  int64_t* plan_total = nullptr;        // [nb]    device-plan scratch
+  int64_t* plan_counts = nullptr;       // [2P] send counts, recv counts
   unsigned long long* check = nullptr;  // [4] verify / check_sorted scratch
-  uint64_t* gather_h = nullptr;         // pinned host mirrors
-  int64_t* place_h = nullptr;
+  int64_t* counts_h = nullptr;          // pinned host mirror of plan_counts
   lsb::Chunking chunking;
   std::vector<int64_t> send_counts, send_displs, recv_counts, recv_displs;
 };
@@ -87,7 +89,6 @@ struct lsb_ctx {
   int64_t launches[LSB_K_COUNT] = {};
   double total_ms[LSB_K_COUNT] = {};
   int64_t scatter_elems = 0;
-  std::vector<int64_t> hist_h;  // [P][nb] as int64 for the planner
 };
 
 namespace {
@@ -227,9 +228,11 @@ int init_rank(lsb_ctx* c, Rank& r, int rank, int dev) {
   }
   LSB_TRY(dev_alloc(&r.gather, std::max(P * nb, P * 4)));
   LSB_TRY(dev_alloc(&r.place, P * nb + P));
+  LSB_TRY(dev_alloc(&r.plan_work, P * nb));
+  LSB_TRY(dev_alloc(&r.plan_total, nb));
+  LSB_TRY(dev_alloc(&r.plan_counts, 2 * P));
   LSB_TRY(dev_alloc(&r.check, 4));
-  LSB_TRY(host_alloc(&r.gather_h, P * nb));
-  LSB_TRY(host_alloc(&r.place_h, P * nb + P));
+  LSB_TRY(host_alloc(&r.counts_h, 2 * P));
   r.send_counts.assign(c->P, 0);
   r.send_displs.assign(c->P, 0);
   r.recv_counts.assign(c->P, 0);
@@ -252,9 +255,11 @@ void free_rank(Rank& r) {
   (void)hipFree(r.first16);
   (void)hipFree(r.gather);
   (void)hipFree(r.place);
+  (void)hipFree(r.plan_work);
+  (void)hipFree(r.plan_total);
+  (void)hipFree(r.plan_counts);
   (void)hipFree(r.check);
-  (void)hipHostFree(r.gather_h);
-  (void)hipHostFree(r.place_h);
+  (void)hipHostFree(r.counts_h);
   if (r.stream) (void)hipStreamDestroy(r.stream);
   r = Rank();
 }
@@ -305,25 +310,31 @@ int digit_counts(lsb_ctx* c, Rank& r, int digit, const uint64_t** counts) {
   return LSB_OK;
 }
 
-// Turn the host plan of rank r into the device placement table.
-int upload_plan(lsb_ctx* c, Rank& r) {
-  const size_t PN = (size_t)c->P * c->nb;
-  int64_t* rend = r.place_h + PN;
-  int64_t acc = 0;
-  for (int s = 0; s < c->P; ++s) {
-    acc += r.recv_counts[s];
-    rend[s] = acc;
-  }
+// Device plan of rank r from its gathered count matrix (r.gather): the
+// placement table stays on the device; only the 2P send/recv counts come
+// back (RCCL takes host counts).  Call plan_fetch after a stream sync.
+int plan_launch(lsb_ctx* c, Rank& r) {
   HIP_TRY(hipSetDevice(r.dev));
-  HIP_TRY(hipMemcpyAsync(r.place, r.place_h, sizeof(int64_t) * (PN + c->P), hipMemcpyHostToDevice,
-                         r.stream));
+  {
+    Timer t(c, &r, LSB_K_EXCHANGE);
+    HIP_TRY(lsb::launch_plan(r.gather, c->P, c->nb, r.rank, c->n, r.plan_work, r.plan_total,
+                             r.place, r.plan_counts, r.stream));
+  }
+  HIP_TRY(hipMemcpyAsync(r.counts_h, r.plan_counts, sizeof(int64_t) * 2 * c->P,
+                         hipMemcpyDeviceToHost, r.stream));
   return LSB_OK;
 }
 
-int plan_rank(lsb_ctx* c, Rank& r) {
-  return lsb_plan_exchange(c->n, c->P, r.rank, c->nb, c->hist_h.data(), r.send_counts.data(),
-                           r.send_displs.data(), r.recv_counts.data(), r.recv_displs.data(),
-                           r.place_h);
+void plan_fetch(lsb_ctx* c, Rank& r) {
+  int64_t sd = 0, rd = 0;
+  for (int q = 0; q < c->P; ++q) {
+    r.send_counts[q] = r.counts_h[q];
+    r.recv_counts[q] = r.counts_h[c->P + q];
+    r.send_displs[q] = sd;
+    r.recv_displs[q] = rd;
+    sd += r.send_counts[q];
+    rd += r.recv_counts[q];
+  }
 }
 
 // R -> B by the plan, then swap: A holds the pass result.
@@ -342,22 +353,25 @@ int place_rank(lsb_ctx* c, Rank& r, int shift) {
 int exchange_loopback(lsb_ctx* c, int digit) {
   const int shift = digit * c->bits;
   const size_t nb = (size_t)c->nb;
-  // counts of every rank -> host (stands in for ncclAllGather)
-  for (Rank& r : c->ranks) {
-    const uint64_t* counts = nullptr;
-    LSB_TRY(digit_counts(c, r, digit, &counts));
-    HIP_TRY(hipMemcpyAsync(r.gather_h, counts, sizeof(uint64_t) * nb, hipMemcpyDeviceToHost,
-                           r.stream));
-  }
+  // counts of every rank into every rank's gather matrix (the device copies
+  // stand in for ncclAllGather), then every rank's device plan.
+  std::vector<const uint64_t*> counts(c->ranks.size(), nullptr);
+  for (Rank& r : c->ranks) LSB_TRY(digit_counts(c, r, digit, &counts[r.rank]));
   for (Rank& r : c->ranks) {
     HIP_TRY(hipSetDevice(r.dev));
     HIP_TRY(hipStreamSynchronize(r.stream));
   }
-  for (Rank& r : c->ranks)
-    for (size_t b = 0; b < nb; ++b) c->hist_h[(size_t)r.rank * nb + b] = (int64_t)r.gather_h[b];
+  for (Rank& q : c->ranks) {
+    HIP_TRY(hipSetDevice(q.dev));
+    for (Rank& s : c->ranks)
+      HIP_TRY(hipMemcpyAsync(q.gather + (size_t)s.rank * nb, counts[s.rank], sizeof(uint64_t) * nb,
+                             hipMemcpyDefault, q.stream));
+    LSB_TRY(plan_launch(c, q));
+  }
   for (Rank& r : c->ranks) {
-    LSB_TRY(plan_rank(c, r));
-    LSB_TRY(upload_plan(c, r));
+    HIP_TRY(hipSetDevice(r.dev));
+    HIP_TRY(hipStreamSynchronize(r.stream));
+    plan_fetch(c, r);
   }
   // all-to-all-v: segment q of rank s's digit-ordered A -> rank q's R.
   for (Rank& q : c->ranks) {
@@ -395,12 +409,9 @@ int exchange_rccl(lsb_ctx* c, int digit) {
     Timer t(c, &r, LSB_K_EXCHANGE);
     RCCL_TRY(ncclAllGather(counts, r.gather, nb, ncclUint64, c->comm, r.stream));
   }
-  HIP_TRY(hipMemcpyAsync(r.gather_h, r.gather, sizeof(uint64_t) * (size_t)P * nb,
-                         hipMemcpyDeviceToHost, r.stream));
+  LSB_TRY(plan_launch(c, r));
   HIP_TRY(hipStreamSynchronize(r.stream));
-  for (size_t i = 0; i < (size_t)P * nb; ++i) c->hist_h[i] = (int64_t)r.gather_h[i];
-  LSB_TRY(plan_rank(c, r));
-  LSB_TRY(upload_plan(c, r));
+  plan_fetch(c, r);
   {
     Timer t(c, &r, LSB_K_EXCHANGE);
     const int me = r.rank;
@@ -447,7 +458,6 @@ lsb_ctx* new_ctx(int64_t n_total, int num_ranks, int radix_bits) {
   c->per = div_ceil(n_total, num_ranks);
   c->bits = radix_bits;
   c->nb = 1 << radix_bits;
-  c->hist_h.assign((size_t)num_ranks * c->nb, 0);
   return c;
 }
 

@@ -226,6 +226,19 @@ def test_large_verify_on_device(lsb_built, n, P):
         assert w.check_sorted()
 
 
+def test_beyond_32bit_indices(lsb_built):
+    """2^32 + 12345 records on one rank (137 GB of A + B): every index,
+    chunk offset and bucket start must be 64-bit (the reference's int MPI
+    counts cap a rank below 2^31 records, mpi/mpi_lsbsort.cpp:257-325)."""
+    n = (1 << 32) + 12345
+    with lsb_built.World(n, ranks=1) as w:
+        w.generate()
+        w.my_sort()
+        assert w.verify() == (True, -1)
+        tail = w.copy_out(0, n - 4, 4)
+        assert np.all(np.diff(tail["key"].astype(np.float64)) >= 0)
+
+
 # ------------------------------------------------------------- the harness
 def test_harness_matches_reference_lines(lsb_built, ref_vectors):
     case = next(c for c in ref_vectors["cases"] if c["n"] == 1000003 and c["P"] == 4)

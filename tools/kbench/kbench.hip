@@ -260,6 +260,11 @@ int main(int argc, char** argv) {
     fflush(stdout);
   };
 
+  run_variant("carry 256x16 G512", 512, k_scatter<256, 16>, 256, 4096, true);
+  run_variant("carry 1024x8 G256", 256, k_scatter<1024, 8>, 1024, 8192, true);
+  run_variant("carry 512x16 G256", 256, k_scatter<512, 16>, 512, 8192, true);
+  run_variant("carry 512x8 G512", 512, k_scatter<512, 8>, 512, 4096, true);
+  run_variant("carry 256x8 G1024", 1024, k_scatter<256, 8>, 256, 2048, true);
   run_variant("v256x16 pf SEQ", 512, k_scatter_v<256, 16, true, true, 2>, 256, 4096, false);
   {
     float ms = time_ms([&] { hipLaunchKernelGGL((k_copy8<256, 8>), dim3((unsigned)(m / 2048)), dim3(256), 0, 0, b.in, b.out, m); }, reps);
