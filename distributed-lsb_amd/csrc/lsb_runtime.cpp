@@ -814,6 +814,51 @@ int lsb_get_scatter_elems(lsb_ctx_t* c, int64_t* elems) {
 //   gstart[b][s] = sum_{b'<b} total[b'] + sum_{s'<s} hist[s'][b]
 // (GlobalCounts[digit*P + rank] scanned, mpi/mpi_lsbsort.cpp:350,378,401-412),
 // and owner(g) = g / per (globalIdxToLocalIdx, mpi/mpi_lsbsort.cpp:113-120).
+int lsb_plan_exchange_device(int dev, int64_t n_total, int P, int me, int nb, const int64_t* hist,
+                             int64_t* send_counts, int64_t* send_displs, int64_t* recv_counts,
+                             int64_t* recv_displs, int64_t* place_off) {
+  if (P < 1 || P > 64 || me < 0 || me >= P || nb < 1 || n_total < 0 || !hist || !send_counts ||
+      !send_displs || !recv_counts || !recv_displs || !place_off)
+    return fail(LSB_ERR_INVALID, "lsb_plan_exchange_device", "arguments");
+  const size_t PN = (size_t)P * nb;
+  for (size_t i = 0; i < PN; ++i)
+    if (hist[i] < 0) return fail(LSB_ERR_INVALID, "lsb_plan_exchange_device", "negative count");
+  HIP_TRY(hipSetDevice(dev));
+  uint64_t* d_hist = nullptr;
+  int64_t *d_work = nullptr, *d_total = nullptr, *d_place = nullptr, *d_counts = nullptr;
+  int rc = LSB_OK;
+  if ((rc = dev_alloc(&d_hist, PN)) == LSB_OK && (rc = dev_alloc(&d_work, PN)) == LSB_OK &&
+      (rc = dev_alloc(&d_total, (size_t)nb)) == LSB_OK && (rc = dev_alloc(&d_place, PN + P)) == LSB_OK &&
+      (rc = dev_alloc(&d_counts, 2 * (size_t)P)) == LSB_OK) {
+    std::vector<int64_t> counts(2 * (size_t)P);
+    hipError_t e = hipMemcpy(d_hist, hist, sizeof(int64_t) * PN, hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+      e = lsb::launch_plan(d_hist, P, nb, me, n_total, d_work, d_total, d_place, d_counts, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(place_off, d_place, sizeof(int64_t) * PN, hipMemcpyDeviceToHost);
+    if (e == hipSuccess)
+      e = hipMemcpy(counts.data(), d_counts, sizeof(int64_t) * 2 * P, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) {
+      rc = fail(LSB_ERR_HIP, "lsb_plan_exchange_device", hipGetErrorString(e));
+    } else {
+      int64_t sd = 0, rd = 0;
+      for (int q = 0; q < P; ++q) {
+        send_counts[q] = counts[q];
+        recv_counts[q] = counts[P + q];
+        send_displs[q] = sd;
+        recv_displs[q] = rd;
+        sd += counts[q];
+        rd += counts[P + q];
+      }
+    }
+  }
+  (void)hipFree(d_hist);
+  (void)hipFree(d_work);
+  (void)hipFree(d_total);
+  (void)hipFree(d_place);
+  (void)hipFree(d_counts);
+  return rc;
+}
+
 int lsb_plan_exchange(int64_t n_total, int P, int me, int nb, const int64_t* hist,
                       int64_t* send_counts, int64_t* send_displs, int64_t* recv_counts,
                       int64_t* recv_displs, int64_t* place_off) {

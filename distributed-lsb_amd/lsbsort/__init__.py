@@ -89,6 +89,7 @@ def _lib() -> ctypes.CDLL:
             "lsb_reset_kernel_stats": (i32, [vp]),
             "lsb_get_scatter_elems": (i32, [vp, P64]),
             "lsb_plan_exchange": (i32, [i64, i32, i32, i32, vp, vp, vp, vp, vp, vp]),
+            "lsb_plan_exchange_device": (i32, [i32, i64, i32, i32, i32, vp, vp, vp, vp, vp, vp]),
             "lsb_strerror": (cp, [i32]),
         }
         for name, (res, args) in sig.items():
@@ -118,8 +119,9 @@ def get_unique_id() -> bytes:
     return buf.raw
 
 
-def plan_exchange(n: int, P: int, rank: int, hist: np.ndarray) -> dict:
-    """Host planner of rank `rank` for a P x nbuckets count matrix."""
+def plan_exchange(n: int, P: int, rank: int, hist: np.ndarray, device: Optional[int] = None) -> dict:
+    """Exchange plan of rank `rank` for a P x nbuckets count matrix: the host
+    planner, or (device=d) the device kernels the runtime runs."""
     hist = np.ascontiguousarray(hist, dtype=np.int64)
     if hist.ndim != 2 or hist.shape[0] != P:
         raise ValueError("hist must be P x nbuckets")
@@ -127,10 +129,13 @@ def plan_exchange(n: int, P: int, rank: int, hist: np.ndarray) -> dict:
     out = {k: np.zeros(P, dtype=np.int64) for k in
            ("send_counts", "send_displs", "recv_counts", "recv_displs")}
     out["place_off"] = np.zeros((P, nb), dtype=np.int64)
-    _check(_lib().lsb_plan_exchange(
-        n, P, rank, nb, hist.ctypes.data, out["send_counts"].ctypes.data,
-        out["send_displs"].ctypes.data, out["recv_counts"].ctypes.data,
-        out["recv_displs"].ctypes.data, out["place_off"].ctypes.data), "lsb_plan_exchange")
+    args = (n, P, rank, nb, hist.ctypes.data, out["send_counts"].ctypes.data,
+            out["send_displs"].ctypes.data, out["recv_counts"].ctypes.data,
+            out["recv_displs"].ctypes.data, out["place_off"].ctypes.data)
+    if device is None:
+        _check(_lib().lsb_plan_exchange(*args), "lsb_plan_exchange")
+    else:
+        _check(_lib().lsb_plan_exchange_device(device, *args), "lsb_plan_exchange_device")
     return out
 
 

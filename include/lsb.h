@@ -161,6 +161,15 @@ int  lsb_plan_exchange(int64_t n_total, int num_ranks, int rank, int nbuckets,
                        int64_t* recv_counts, int64_t* recv_displs,
                        int64_t* place_off);
 
+/* The same plan computed by the device kernels the runtime uses (it keeps
+ * place_off on the GPU and fetches only the 2P counts); host arrays in and
+ * out, on device `dev_id`.  For testing the two planners against each other. */
+int  lsb_plan_exchange_device(int dev_id, int64_t n_total, int num_ranks, int rank, int nbuckets,
+                              const int64_t* hist,
+                              int64_t* send_counts, int64_t* send_displs,
+                              int64_t* recv_counts, int64_t* recv_displs,
+                              int64_t* place_off);
+
 const char* lsb_strerror(int code);
 
 #ifdef __cplusplus

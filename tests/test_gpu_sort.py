@@ -216,6 +216,38 @@ def test_kernel_stats(lsb_built):
         assert w.scatter_elems() == 8 << 20
 
 
+def _rebalanced_hist(rng, P, nb, n, here, skew):
+    """Random P x nb count matrix whose row r sums to here(n, P, r)."""
+    if skew:
+        p = rng.dirichlet(np.full(nb, 0.05))
+    else:
+        p = np.full(nb, 1.0 / nb)
+    return np.stack([rng.multinomial(here[r], p) for r in range(P)]).astype(np.int64)
+
+
+@pytest.mark.parametrize("P,nb,n,skew", [(1, 256, 10_000, False), (2, 256, 0, False),
+                                          (3, 256, 7, True), (5, 65536, 1_000_003, False),
+                                          (7, 256, 100_000, True), (8, 65536, 5_000_000, True),
+                                          (64, 256, 1_000, False)])
+def test_device_plan_equals_host_plan(lsb_built, P, nb, n, skew):
+    """The runtime's device planner (k_plan_*) against the host planner."""
+    rng = np.random.default_rng(P * 1000 + nb + n)
+    here = [lsb_built.here(n, P, r) for r in range(P)]
+    hist = _rebalanced_hist(rng, P, nb, n, here, skew)
+    for me in range(P):
+        h = lsb_built.plan_exchange(n, P, me, hist)
+        d = lsb_built.plan_exchange(n, P, me, hist, device=0)
+        for k in ("send_counts", "send_displs", "recv_counts", "recv_displs"):
+            assert np.array_equal(h[k], d[k]), (me, k)
+        # offsets matter only where a piece of (s, b) lands in my range
+        gstart = np.concatenate([[0], np.cumsum(hist.sum(0))[:-1]])[None, :] + \
+            np.concatenate([np.zeros((1, nb), np.int64), np.cumsum(hist, 0)[:-1]])
+        per = -(-n // P) if n else 0
+        lo, hi = me * per, me * per + here[me]
+        live = (np.minimum(gstart + hist, hi) - np.maximum(gstart, lo)) > 0
+        assert np.array_equal(h["place_off"][live], d["place_off"][live])
+
+
 # ------------------------------------------------------------ larger sizes
 @pytest.mark.parametrize("n,P", [(1 << 27, 1), ((1 << 26) + 12345, 2)])
 def test_large_verify_on_device(lsb_built, n, P):
