@@ -1,0 +1,31 @@
+"""Per-kernel time of one single-rank sort (development tool).
+
+python tools/digit_probe.py [log2 n]  -> ms per sort by kernel, and verify.
+Used for the kernel-variant A/B runs recorded in DESIGN.md §5.
+"""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "distributed-lsb_amd"))
+import lsbsort  # noqa: E402
+
+lg = int(sys.argv[1]) if len(sys.argv) > 1 else 30
+n = 1 << lg
+w = lsbsort.World(n, 1)
+w.set_timing(True)
+names = ["upsweep", "scan", "scatter", "exchange", "place", "sort"]
+for rep in range(2):
+    w.generate()
+    w.my_sort()
+    w.sync()
+    w.generate()
+    w.reset_kernel_stats()
+    t0 = time.perf_counter()
+    w.my_sort()
+    w.sync()
+    wall = (time.perf_counter() - t0) * 1e3
+    st = w.kernel_stats()
+    ok = w.verify()
+    parts = " ".join(f"{k}={st[k][1]:.2f}ms/{st[k][0]}" for k in names if st[k][0])
+    print(f"n=2^{lg} wall={wall:.2f}ms {n / wall / 1e3:.0f} Melem/s verify={ok} {parts}", flush=True)
