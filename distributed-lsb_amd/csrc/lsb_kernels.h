@@ -52,8 +52,10 @@ hipError_t launch_digit16_counts(const Elem* A, int64_t m, int shift, int64_t* f
                                  uint64_t* counts, hipStream_t s);
 
 // chunk_hist[b * G + c] = number of elements of chunk c whose digit is b.
+// span (optional, 2 words, OR-accumulated): span[0] |= OR of the keys,
+// span[1] |= OR of their complements.
 hipError_t launch_upsweep(const Elem* A, int64_t m, int shift, Chunking ch,
-                          uint32_t* chunk_hist, hipStream_t s);
+                          uint32_t* chunk_hist, uint64_t* span, hipStream_t s);
 
 // chunk_off[b * G + c] = sum_{c' < c} chunk_hist[b * G + c'];  totals[b] = row sum.
 hipError_t launch_scan(const uint32_t* chunk_hist, int G, uint64_t* chunk_off,

@@ -182,12 +182,19 @@ __global__ __launch_bounds__(256) void k_pcg_fill(Elem* __restrict__ A, int64_t 
 // ballot-match aggregation; tools/kbench/upsweep.hip).  A wave whose 64
 // digits are all equal (sorted or skewed input) adds once instead of
 // serialising 64 same-address atomics.
-template <int BLOCK, int IPT>
+//
+// SPAN (first pass of lsb_sort only): also OR-reduce the keys and their
+// complements into span[0], span[1]; bit i of span[0] & span[1] is set iff
+// keys differ in bit i.  Digits with no such bit are skipped.
+template <int BLOCK, int IPT, bool SPAN>
 __global__ __launch_bounds__(BLOCK) void k_upsweep(const Elem* __restrict__ A, int64_t m,
                                                    int shift, int64_t chunk_elems, int G,
-                                                   uint32_t* __restrict__ chunk_hist) {
+                                                   uint32_t* __restrict__ chunk_hist,
+                                                   unsigned long long* __restrict__ span) {
   constexpr int W = BLOCK / 64;
   __shared__ uint32_t hist[W][kBuckets];
+  __shared__ uint64_t span_or[W], span_nor[W];
+  uint64_t kor = 0, knor = 0;
   for (int i = threadIdx.x; i < W * kBuckets; i += BLOCK) (&hist[0][0])[i] = 0;
   __syncthreads();
   const int w = threadIdx.x >> 6;
@@ -208,6 +215,10 @@ __global__ __launch_bounds__(BLOCK) void k_upsweep(const Elem* __restrict__ A, i
     for (int i = 0; i < IPT; ++i) {
       const int64_t idx = tb + (int64_t)i * BLOCK + threadIdx.x;
       const bool valid = idx < end;
+      if (SPAN && valid) {
+        kor |= k[i];
+        knor |= ~k[i];
+      }
       const uint32_t d = (uint32_t)(k[i] >> shift) & (kBuckets - 1);
       const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
       if (__all(valid && d == d0)) {
@@ -223,6 +234,28 @@ __global__ __launch_bounds__(BLOCK) void k_upsweep(const Elem* __restrict__ A, i
 #pragma unroll
     for (int ww = 0; ww < W; ++ww) s += hist[ww][b];
     chunk_hist[(int64_t)b * G + c] = s;
+  }
+  if (SPAN) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      kor |= __shfl_xor(kor, off, 64);
+      knor |= __shfl_xor(knor, off, 64);
+    }
+    if (lane_id() == 0) {
+      span_or[w] = kor;
+      span_nor[w] = knor;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint64_t o = 0, no = 0;
+#pragma unroll
+      for (int ww = 0; ww < W; ++ww) {
+        o |= span_or[ww];
+        no |= span_nor[ww];
+      }
+      atomicOr(&span[0], (unsigned long long)o);
+      atomicOr(&span[1], (unsigned long long)no);
+    }
   }
 }
 
@@ -732,10 +765,15 @@ hipError_t launch_digit16_counts(const Elem* A, int64_t m, int shift, int64_t* f
 }
 
 hipError_t launch_upsweep(const Elem* A, int64_t m, int shift, Chunking ch, uint32_t* chunk_hist,
-                          hipStream_t s) {
+                          uint64_t* span, hipStream_t s) {
   if (m <= 0) return hipSuccess;
-  hipLaunchKernelGGL((k_upsweep<256, 16>), dim3(ch.num_chunks), dim3(256), 0, s, A, m, shift,
-                     ch.chunk_elems, ch.num_chunks, chunk_hist);
+  if (span)
+    hipLaunchKernelGGL((k_upsweep<256, 16, true>), dim3(ch.num_chunks), dim3(256), 0, s, A, m,
+                       shift, ch.chunk_elems, ch.num_chunks, chunk_hist,
+                       reinterpret_cast<unsigned long long*>(span));
+  else
+    hipLaunchKernelGGL((k_upsweep<256, 16, false>), dim3(ch.num_chunks), dim3(256), 0, s, A, m,
+                       shift, ch.chunk_elems, ch.num_chunks, chunk_hist, nullptr);
   return hipGetLastError();
 }
 

@@ -64,6 +64,9 @@ struct Rank {
   int64_t* plan_total = nullptr;        // [nb]    device-plan scratch
   int64_t* plan_counts = nullptr;       // [2P] send counts, recv counts
   unsigned long long* check = nullptr;  // [4] verify / check_sorted scratch
+  uint64_t* span = nullptr;             // [2] OR of keys, OR of ~keys (first pass of lsb_sort)
+  uint64_t* span_gather = nullptr;      // [2P] all-gathered spans (RCCL)
+  uint64_t* span_h = nullptr;           // [2P] pinned host mirror
   int64_t* counts_h = nullptr;          // pinned host mirror of plan_counts
   lsb::Chunking chunking;
   std::vector<int64_t> send_counts, send_displs, recv_counts, recv_displs;
@@ -83,6 +86,11 @@ struct lsb_ctx {
   ncclComm_t comm = nullptr;
   bool timing = false;
   bool force_exchange = false;
+  bool skip_constant = true;  // lsb_sort skips digits on which all keys agree
+  // What the last lsb_sort ran (lsb_get_last_sort).
+  int last_local_passes = 0;
+  int last_exchanges = 0;
+  uint64_t last_varying = 0;
   lsb::KeyGen keygen;
   std::vector<PendingEvent> pending;
   std::vector<hipEvent_t> event_pool;
@@ -232,6 +240,9 @@ int init_rank(lsb_ctx* c, Rank& r, int rank, int dev) {
   LSB_TRY(dev_alloc(&r.plan_total, nb));
   LSB_TRY(dev_alloc(&r.plan_counts, 2 * P));
   LSB_TRY(dev_alloc(&r.check, 4));
+  LSB_TRY(dev_alloc(&r.span, 2));
+  LSB_TRY(dev_alloc(&r.span_gather, 2 * P));
+  LSB_TRY(host_alloc(&r.span_h, 2 * P));
   LSB_TRY(host_alloc(&r.counts_h, 2 * P));
   r.send_counts.assign(c->P, 0);
   r.send_displs.assign(c->P, 0);
@@ -259,6 +270,9 @@ void free_rank(Rank& r) {
   (void)hipFree(r.plan_total);
   (void)hipFree(r.plan_counts);
   (void)hipFree(r.check);
+  (void)hipFree(r.span);
+  (void)hipFree(r.span_gather);
+  (void)hipHostFree(r.span_h);
   (void)hipHostFree(r.counts_h);
   if (r.stream) (void)hipStreamDestroy(r.stream);
   r = Rank();
@@ -271,7 +285,7 @@ Rank* local_rank(lsb_ctx* c, int rank) {
 }
 
 // ---- one local stable 8-bit pass A -> B, then swap (localShuffle) -------
-int local_pass(lsb_ctx* c, Rank& r, int shift) {
+int local_pass(lsb_ctx* c, Rank& r, int shift, bool want_span = false) {
   HIP_TRY(hipSetDevice(r.dev));
   if (r.here == 0) {
     HIP_TRY(hipMemsetAsync(r.totals, 0, sizeof(uint64_t) * lsb::kBuckets, r.stream));
@@ -280,7 +294,8 @@ int local_pass(lsb_ctx* c, Rank& r, int shift) {
   const lsb::Chunking& ch = r.chunking;
   {
     Timer t(c, &r, LSB_K_UPSWEEP);
-    HIP_TRY(lsb::launch_upsweep(r.A, r.here, shift, ch, r.chunk_hist, r.stream));
+    HIP_TRY(lsb::launch_upsweep(r.A, r.here, shift, ch, r.chunk_hist,
+                                want_span ? r.span : nullptr, r.stream));
   }
   {
     Timer t(c, &r, LSB_K_SCAN);
@@ -437,10 +452,19 @@ int exchange_rccl(lsb_ctx* c, int digit) {
   return place_rank(c, r, shift);
 }
 
-int do_pass(lsb_ctx* c, int digit) {
-  for (int sub = 0; sub < c->bits / lsb::kDigitBits; ++sub)
-    for (Rank& r : c->ranks) LSB_TRY(local_pass(c, r, digit * c->bits + sub * lsb::kDigitBits));
+// One exchange digit: its 8-bit local sub-passes, then (P > 1) the exchange.
+// varying: key bits that differ somewhere; a sub-pass whose byte is constant
+// is the identity and is skipped (all ~0 = run everything).  want_span: the
+// first sub-pass also reduces the key span (lsb_sort, digit 0).
+int do_pass(lsb_ctx* c, int digit, uint64_t varying = ~0ull, bool want_span = false) {
+  for (int sub = 0; sub < c->bits / lsb::kDigitBits; ++sub) {
+    const int shift = digit * c->bits + sub * lsb::kDigitBits;
+    if (!want_span && ((varying >> shift) & (lsb::kBuckets - 1)) == 0) continue;
+    for (Rank& r : c->ranks) LSB_TRY(local_pass(c, r, shift, want_span && sub == 0));
+    ++c->last_local_passes;
+  }
   if (!exchanging(c)) return LSB_OK;
+  ++c->last_exchanges;
   if (c->mode == Mode::kRccl) return exchange_rccl(c, digit);
   return exchange_loopback(c, digit);
 }
@@ -501,6 +525,36 @@ int allreduce_min_i64(lsb_ctx* c, int64_t* v) {
   RCCL_TRY(ncclAllReduce(d, d, 1, ncclInt64, ncclMin, c->comm, r.stream));
   HIP_TRY(hipMemcpyAsync(v, d, sizeof(int64_t), hipMemcpyDeviceToHost, r.stream));
   HIP_TRY(hipStreamSynchronize(r.stream));
+  return LSB_OK;
+}
+
+// Global key span after the first pass: OR of all keys and of their
+// complements over every rank (RCCL: all-gather of the 2 words per rank).
+int gather_span(lsb_ctx* c, uint64_t* kor, uint64_t* knor) {
+  *kor = *knor = 0;
+  if (c->mode == Mode::kRccl) {
+    Rank& r = c->ranks[0];
+    HIP_TRY(hipSetDevice(r.dev));
+    RCCL_TRY(ncclAllGather(r.span, r.span_gather, 2, ncclUint64, c->comm, r.stream));
+    HIP_TRY(hipMemcpyAsync(r.span_h, r.span_gather, sizeof(uint64_t) * 2 * c->P,
+                           hipMemcpyDeviceToHost, r.stream));
+    HIP_TRY(hipStreamSynchronize(r.stream));
+    for (int q = 0; q < c->P; ++q) {
+      *kor |= r.span_h[2 * q];
+      *knor |= r.span_h[2 * q + 1];
+    }
+    return LSB_OK;
+  }
+  for (Rank& r : c->ranks) {
+    HIP_TRY(hipSetDevice(r.dev));
+    HIP_TRY(hipMemcpyAsync(r.span_h, r.span, sizeof(uint64_t) * 2, hipMemcpyDeviceToHost, r.stream));
+  }
+  for (Rank& r : c->ranks) {
+    HIP_TRY(hipSetDevice(r.dev));
+    HIP_TRY(hipStreamSynchronize(r.stream));
+    *kor |= r.span_h[0];
+    *knor |= r.span_h[1];
+  }
   return LSB_OK;
 }
 
@@ -624,6 +678,9 @@ int lsb_set_option(lsb_ctx_t* c, int option, int64_t value) {
       }
       c->force_exchange = value != 0;
       return LSB_OK;
+    case LSB_OPT_SKIP_CONSTANT_DIGITS:
+      c->skip_constant = value != 0;
+      return LSB_OK;
     default:
       return fail(LSB_ERR_INVALID, "lsb_set_option", "unknown option");
   }
@@ -697,8 +754,36 @@ int lsb_sort(lsb_ctx_t* c) {
   sort_timers.reserve(c->ranks.size());
   for (Rank& r : c->ranks) sort_timers.emplace_back(c, &r, LSB_K_SORT);
   const int passes = 64 / c->bits;
-  for (int d = 0; d < passes; ++d) LSB_TRY(do_pass(c, d));
+  c->last_local_passes = c->last_exchanges = 0;
+  c->last_varying = ~0ull;
+  if (!c->skip_constant) {
+    for (int d = 0; d < passes; ++d) LSB_TRY(do_pass(c, d));
+  } else {
+    for (Rank& r : c->ranks) {
+      HIP_TRY(hipSetDevice(r.dev));
+      HIP_TRY(hipMemsetAsync(r.span, 0, 2 * sizeof(uint64_t), r.stream));
+    }
+    LSB_TRY(do_pass(c, 0, ~0ull, true));
+    uint64_t kor = 0, knor = 0;
+    LSB_TRY(gather_span(c, &kor, &knor));
+    c->last_varying = kor & knor;
+    const uint64_t digit_mask = (1ull << c->bits) - 1;
+    for (int d = 1; d < passes; ++d) {
+      // A digit on which every key agrees: the stable pass and the exchange
+      // (order (digit, rank) = rank order) are both the identity.
+      if (((c->last_varying >> (d * c->bits)) & digit_mask) == 0) continue;
+      LSB_TRY(do_pass(c, d, c->last_varying));
+    }
+  }
   for (Timer& t : sort_timers) t.stop();
+  return LSB_OK;
+}
+
+int lsb_get_last_sort(lsb_ctx_t* c, int* local_passes, int* exchanges, uint64_t* varying_bits) {
+  LSB_TRY(check_ctx(c));
+  if (local_passes) *local_passes = c->last_local_passes;
+  if (exchanges) *exchanges = c->last_exchanges;
+  if (varying_bits) *varying_bits = c->last_varying;
   return LSB_OK;
 }
 

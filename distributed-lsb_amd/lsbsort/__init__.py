@@ -43,7 +43,7 @@ LSB_ERR_VERIFY = 5
 DIST_UNIFORM, DIST_ZIPF = 0, 1
 K_UPSWEEP, K_SCAN, K_SCATTER, K_EXCHANGE, K_PLACE, K_SORT = range(6)
 KERNEL_NAMES = ("upsweep", "scan", "scatter", "exchange", "place", "sort")
-OPT_TIMING, OPT_FORCE_EXCHANGE = 0, 1
+OPT_TIMING, OPT_FORCE_EXCHANGE, OPT_SKIP_CONSTANT_DIGITS = 0, 1, 2
 
 
 class LsbError(RuntimeError):
@@ -74,6 +74,7 @@ def _lib() -> ctypes.CDLL:
             "lsb_create_rank": (i32, [ctypes.POINTER(vp), i64, i32, i32, i32, i32, ctypes.c_char_p]),
             "lsb_destroy": (None, [vp]),
             "lsb_set_option": (i32, [vp, i32, i64]),
+            "lsb_get_last_sort": (i32, [vp, vp, vp, vp]),
             "lsb_local_ranks": (i32, [vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
             "lsb_generate": (i32, [vp]),
             "lsb_generate_ex": (i32, [vp, i32, ctypes.c_double]),
@@ -295,6 +296,13 @@ class World:
     # -- measurement ----------------------------------------------------------
     def set_timing(self, on: bool = True) -> None:
         self.set_option(OPT_TIMING, 1 if on else 0)
+
+    def last_sort(self) -> tuple:
+        """(local 8-bit passes, exchanges, varying key bits) of the last my_sort."""
+        lp, ex, vb = ctypes.c_int(), ctypes.c_int(), ctypes.c_uint64()
+        _check(_lib().lsb_get_last_sort(self._h, ctypes.byref(lp), ctypes.byref(ex), ctypes.byref(vb)),
+               "lsb_get_last_sort")
+        return int(lp.value), int(ex.value), int(vb.value)
 
     def kernel_stats(self) -> dict:
         out = {}

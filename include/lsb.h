@@ -69,6 +69,8 @@ typedef struct lsb_ctx lsb_ctx_t;
 /* Options for lsb_set_option(). */
 #define LSB_OPT_TIMING          0  /* 1: record HIP events around every kernel */
 #define LSB_OPT_FORCE_EXCHANGE  1  /* 1: run the exchange path even when P == 1 */
+#define LSB_OPT_SKIP_CONSTANT_DIGITS 2  /* 1 (default): lsb_sort skips every digit after
+                                           the first on which all keys agree */
 
 /* ---- geometry: DistributedArray::create (mpi/mpi_lsbsort.cpp:144-149) ---- */
 int64_t lsb_per_rank(int64_t n_total, int num_ranks);            /* ceil(n/P) */
@@ -117,8 +119,18 @@ int  lsb_copy_out(lsb_ctx_t* ctx, int rank, int64_t off, int64_t cnt, lsb_elem_t
 /* ---- the hot path ------------------------------------------------------- */
 /* == mySort(A, B): all 64/radix_bits passes; result in A.  Asynchronous
  * with respect to the host except for the per-pass count exchange when
- * P > 1; call lsb_sync() to wait. */
+ * P > 1 and one 16-byte key-span read after the first pass; call
+ * lsb_sync() to wait.
+ * The first pass's count kernel also reduces the OR of all keys and of their
+ * complements (all-gathered when P > 1).  A later digit on which every key
+ * agrees is skipped: its stable pass and its exchange are the identity, so
+ * the output is unchanged (keys < 2^32 take 4 of 8 passes).  Uniform 64-bit
+ * keys run every pass.  LSB_OPT_SKIP_CONSTANT_DIGITS = 0 turns this off. */
 int  lsb_sort(lsb_ctx_t* ctx);
+/* What the last lsb_sort ran: 8-bit local passes, exchanges (0 when P == 1
+ * and not forced) and the key bits that vary (~0 when skipping is off). */
+int  lsb_get_last_sort(lsb_ctx_t* ctx, int* local_passes, int* exchanges,
+                       uint64_t* varying_bits);
 /* == globalShuffle(A, B, digit): one pass, result in A. */
 int  lsb_pass(lsb_ctx_t* ctx, int digit);
 int  lsb_sync(lsb_ctx_t* ctx);

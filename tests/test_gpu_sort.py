@@ -145,6 +145,72 @@ def test_ragged_and_tiny(lsb_built, oracle_mod, n, P):
     assert np.array_equal(out, oracle_mod.stable_sort(a))
 
 
+# ------------------------------------------------- constant-digit skipping
+def _masked_keys(n, mask, rng):
+    a = np.zeros(n, dtype=DT)
+    a["key"] = rng.integers(0, 2**64 - 1, n, dtype=np.uint64) & np.uint64(mask)
+    a["val"] = np.arange(n, dtype=np.uint64)
+    return a
+
+
+# (key mask, radix bits, P) -> 8-bit local passes and exchanges lsb_sort must run.
+# Digit 0 always runs (the key span comes out of its count kernel).
+@pytest.mark.parametrize("mask,bits,P,passes,exchanges", [
+    (0xFFFFFFFF, 8, 1, 4, 0),                 # keys < 2^32: bytes 4..7 constant
+    (0xFFFF0000000000FF, 8, 1, 3, 0),         # bytes 1..5 constant
+    (0xFFFFFFFFFFFFFFFF, 8, 1, 8, 0),         # nothing to skip
+    (0x0, 8, 1, 1, 0),                        # all keys 0: only the first pass
+    (0x0000000000FFFFFF, 8, 3, 3, 3),         # 3 digits, each with its exchange
+    (0x0000000000FFFFFF, 16, 3, 3, 2),        # 16-bit: digits 0,1; byte 3 skipped
+    (0xFF00000000000000, 16, 4, 3, 2),        # 16-bit: digit 0 always, digit 3 only its high byte
+    (0x00000000FFFF0000, 16, 8, 4, 2),        # digit 0 forced (constant), digit 1 runs
+])
+def test_constant_digits_skipped(lsb_built, oracle_mod, mask, bits, P, passes, exchanges):
+    rng = np.random.default_rng(mask & 0xFFFF ^ P)
+    a = _masked_keys(100_003, mask, rng)
+    with lsb_built.World(a.size, ranks=P, radix_bits=bits) as w:
+        w.scatter_global(a)
+        w.my_sort()
+        assert np.array_equal(w.gather_global(), oracle_mod.stable_sort(a))
+        lp, ex, varying = w.last_sort()
+        assert (lp, ex) == (passes, exchanges)
+        assert varying & ~mask == 0
+
+
+def test_constant_digit_skipping_can_be_disabled(lsb_built, oracle_mod):
+    a = _masked_keys(50_000, 0xFFFF, np.random.default_rng(7))
+    with lsb_built.World(a.size, ranks=2) as w:
+        w.set_option(lsb_built.OPT_SKIP_CONSTANT_DIGITS, 0)
+        w.scatter_global(a)
+        w.my_sort()
+        assert np.array_equal(w.gather_global(), oracle_mod.stable_sort(a))
+        assert w.last_sort() == (8, 8, 2**64 - 1)
+
+
+def test_constant_digits_skipped_over_rccl(lsb_built, oracle_mod):
+    """The span is all-gathered over RCCL before any digit is skipped."""
+    a = _masked_keys(70_001, 0x00FF00FF, np.random.default_rng(11))
+    uid = lsb_built.get_unique_id()
+    w = lsb_built.World.rank(a.size, 1, 0, 0, uid, radix_bits=16)
+    try:
+        w.set_option(lsb_built.OPT_FORCE_EXCHANGE, 1)
+        w.copy_in(0, a, 0)
+        w.my_sort()
+        w.sync()
+        assert np.array_equal(w.copy_out(0), oracle_mod.stable_sort(a))
+        assert w.last_sort()[:2] == (3, 2)  # digit 0 (both bytes), byte 2; digits 0 and 1
+    finally:
+        w.close()
+
+
+def test_uniform_input_runs_every_pass(lsb_built):
+    with lsb_built.World(1 << 20, ranks=1) as w:
+        w.generate()
+        w.my_sort()
+        assert w.last_sort() == (8, 0, 2**64 - 1)
+        assert w.verify() == (True, -1)
+
+
 # ------------------------------------------------------------------ checks
 def test_verify_catches_corruption(lsb_built):
     n, P = 100_000, 2

@@ -223,7 +223,7 @@ int main(int argc, char** argv) {
   // reference result: the no-carry variant (the round-1 product kernel)
   {
     Chunking ch = make_chunking(m, 512);
-    CK(launch_upsweep(b.in, m, shift, ch, b.hist, 0));
+    CK(launch_upsweep(b.in, m, shift, ch, b.hist, nullptr, 0));
     CK(launch_scan(b.hist, ch.num_chunks, b.off, b.tot, 0));
     KFn k0 = k_scatter_v<256, 16, false, false, 2>;
     float t = time_ms([&] { hipLaunchKernelGGL(k0, dim3(ch.num_chunks), dim3(256), 0, 0, b.in, b.ref, m, shift, ch.chunk_elems, ch.num_chunks, b.off, b.tot); }, reps);
@@ -234,7 +234,7 @@ int main(int argc, char** argv) {
     unsigned long long h = 0;
     CK(hipMemcpy(&h, bad, sizeof h, hipMemcpyDeviceToHost));
     printf("product k_scatter (carry)  %8.3f ms  %7.1f GB/s  %s\n", tp, gb / tp * 1e3, h == 0 ? "OK" : "MISMATCH");
-    float tu = time_ms([&] { CK(launch_upsweep(b.in, m, shift, ch, b.hist, 0)); }, reps);
+    float tu = time_ms([&] { CK(launch_upsweep(b.in, m, shift, ch, b.hist, nullptr, 0)); }, reps);
     printf("product k_upsweep          %8.3f ms  %7.1f GB/s (16 B/elt)\n", tu, 16.0 * m / 1e9 / tu * 1e3);
   }
 
@@ -244,7 +244,7 @@ int main(int argc, char** argv) {
     const int64_t tpc = (tiles + max_chunks - 1) / max_chunks;
     ch.chunk_elems = tpc * tile;
     ch.num_chunks = (int)((m + ch.chunk_elems - 1) / ch.chunk_elems);
-    CK(launch_upsweep(b.in, m, shift, ch, b.hist, 0));
+    CK(launch_upsweep(b.in, m, shift, ch, b.hist, nullptr, 0));
     CK(launch_scan(b.hist, ch.num_chunks, b.off, b.tot, 0));
     float t = time_ms([&] {
       hipLaunchKernelGGL(kern, dim3(ch.num_chunks), dim3(block), 0, 0, b.in, b.out, m, shift,

@@ -52,7 +52,7 @@ int main() {
   // one-shot pass (the product)
   Chunking ch = make_chunking(m, 512);
   auto one = [&] {
-    CK(launch_upsweep(in, m, shift, ch, hist, 0));
+    CK(launch_upsweep(in, m, shift, ch, hist, nullptr, 0));
     CK(launch_scan(hist, ch.num_chunks, off, tot, 0));
     CK(launch_scatter(in, ref, m, shift, ch, off, tot, 0));
   };
@@ -65,7 +65,7 @@ int main() {
       auto pass = [&] {
         hipLaunchKernelGGL(k_excl, dim3(1), dim3(1), 0, 0, gtot, base);
         for (int64_t s0 = 0; s0 < m; s0 += sc) {
-          CK(launch_upsweep(in + s0, sc, shift, cs, hist, 0));
+          CK(launch_upsweep(in + s0, sc, shift, cs, hist, nullptr, 0));
           CK(launch_scan(hist, cs.num_chunks, off, tot, 0));
           hipLaunchKernelGGL(k_add_base, dim3(1), dim3(256), 0, 0, off, cs.num_chunks, base, tot);
           CK(launch_scatter(in + s0, out, sc, shift, cs, off, zero, 0));

@@ -89,7 +89,7 @@ int main() {
   std::vector<uint32_t> a(256 * 4096), b(256 * 4096);
   for (int G : {512, 1024, 2048}) {
     Chunking ch = make_chunking(m, G);
-    float t0 = time_ms([&] { CK(launch_upsweep(A, m, 8, ch, h0, 0)); }, 5);
+    float t0 = time_ms([&] { CK(launch_upsweep(A, m, 8, ch, h0, nullptr, 0)); }, 5);
     printf("G=%4d product (match)       %6.3f ms %6.0f GB/s\n", ch.num_chunks, t0, gb / t0 * 1e3);
     auto check = [&](const char* name, auto fn) {
       float t = time_ms(fn, 5);
