@@ -67,10 +67,11 @@ hipError_t launch_scan(const uint32_t* chunk_hist, int G, uint64_t* chunk_off,
 hipError_t launch_scatter(const Elem* in, Elem* out, int64_t m, int shift, Chunking ch,
                           const uint64_t* chunk_off, const uint64_t* totals, hipStream_t s);
 
-// Receiver-side placement after the exchange: recv[k] (from source s, the
-// first s with k < rend[s]) goes to A[place_off[s * nbuckets + digit] + k].
-hipError_t launch_place(const Elem* recv, Elem* A, int64_t m, int shift, int nbuckets, int P,
-                        const int64_t* rend, const int64_t* place_off, hipStream_t s);
+// Receiver-side placement of one source's received range: src[i] (receive
+// index k0 + i) goes to out[off_row[digit] + k0 + i], off_row = the source's
+// row of the placement table (place_off[s * nbuckets ...]).
+hipError_t launch_place(const Elem* src, Elem* out, int64_t k0, int64_t count, int shift,
+                        int nbuckets, const int64_t* off_row, hipStream_t s);
 
 // Exchange plan of rank `me` on device from the all-gathered counts
 // hist[s * nb + b] (same rule as the host planner lsb_plan_exchange):

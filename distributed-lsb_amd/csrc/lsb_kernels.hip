@@ -453,45 +453,42 @@ __global__ __launch_bounds__(BLOCK, 2) void k_scatter(const Elem* __restrict__ i
 // ------------------------------------------------------------------- place
 constexpr int kPlaceBlock = 256;
 constexpr int kPlaceIpt = 8;
-constexpr int kPlaceLdsEntries = 4096;  // P * nbuckets offsets (32 KiB) staged in LDS up to here
+constexpr int kPlaceLdsBuckets = 4096;  // offset rows up to here (32 KiB) are staged in LDS
 
+// One source's received range: record k in [k0, k0 + count) of the receive
+// order (src[k - k0]) goes to out[off[digit] + k], off = that source's row of
+// the placement table.  The exchange launches it per source and per slice,
+// so a slice is placed while the next one is still in flight.
 template <bool kLds>
-__global__ __launch_bounds__(kPlaceBlock) void k_place(const Elem* __restrict__ recv,
-                                                       Elem* __restrict__ A, int64_t m, int shift,
-                                                       uint32_t mask, int P,
-                                                       const int64_t* __restrict__ rend,
-                                                       const int64_t* __restrict__ place_off) {
-  __shared__ int64_t lds_off[kLds ? kPlaceLdsEntries : 1];
-  __shared__ int64_t lds_end[kLds ? 64 : 1];
+__global__ __launch_bounds__(kPlaceBlock) void k_place(const Elem* __restrict__ src,
+                                                       Elem* __restrict__ out, int64_t k0,
+                                                       int64_t count, int shift, uint32_t mask,
+                                                       const int64_t* __restrict__ off_row) {
+  __shared__ int64_t lds_off[kLds ? kPlaceLdsBuckets : 1];
   const int nb = (int)mask + 1;
-  const int64_t* off = place_off;
-  const int64_t* ends = rend;
+  const int64_t* off = off_row;
   if (kLds) {
-    for (int i = threadIdx.x; i < P * nb; i += kPlaceBlock) lds_off[i] = place_off[i];
-    for (int i = threadIdx.x; i < P; i += kPlaceBlock) lds_end[i] = rend[i];
+    for (int i = threadIdx.x; i < nb; i += kPlaceBlock) lds_off[i] = off_row[i];
     __syncthreads();
     off = lds_off;
-    ends = lds_end;
   }
   // kPlaceIpt records in flight per thread (a 1-record grid-stride loop
   // reached 4.4 TB/s; streaming copies need several loads outstanding).
   const int64_t step = (int64_t)gridDim.x * kPlaceBlock * kPlaceIpt;
-  for (int64_t base = (int64_t)blockIdx.x * kPlaceBlock * kPlaceIpt + threadIdx.x; base < m;
+  for (int64_t base = (int64_t)blockIdx.x * kPlaceBlock * kPlaceIpt + threadIdx.x; base < count;
        base += step) {
     Elem x[kPlaceIpt];
 #pragma unroll
     for (int i = 0; i < kPlaceIpt; ++i) {
       const int64_t k = base + (int64_t)i * kPlaceBlock;
-      x[i] = k < m ? load_elem(recv + k) : Elem{0ull, 0ull};
+      x[i] = k < count ? load_elem(src + k) : Elem{0ull, 0ull};
     }
 #pragma unroll
     for (int i = 0; i < kPlaceIpt; ++i) {
       const int64_t k = base + (int64_t)i * kPlaceBlock;
-      if (k < m) {
-        int s = 0;
-        while (s < P - 1 && k >= ends[s]) ++s;  // first source whose segment holds k
+      if (k < count) {
         const uint32_t d = (uint32_t)(x[i].key >> shift) & mask;
-        store_elem(A + (off[(int64_t)s * nb + d] + k), x[i]);
+        store_elem(out + (off[d] + k0 + k), x[i]);
       }
     }
   }
@@ -795,18 +792,18 @@ hipError_t launch_scatter(const Elem* in, Elem* out, int64_t m, int shift, Chunk
   return hipGetLastError();
 }
 
-hipError_t launch_place(const Elem* recv, Elem* A, int64_t m, int shift, int nbuckets, int P,
-                        const int64_t* rend, const int64_t* place_off, hipStream_t s) {
-  if (m <= 0) return hipSuccess;
-  if (P < 1 || P > 64 || (nbuckets != 256 && nbuckets != 65536)) return hipErrorInvalidValue;
-  const dim3 grid(grid_for(m, kPlaceBlock, 4096));
+hipError_t launch_place(const Elem* src, Elem* out, int64_t k0, int64_t count, int shift,
+                        int nbuckets, const int64_t* off_row, hipStream_t s) {
+  if (count <= 0) return hipSuccess;
+  if (nbuckets != 256 && nbuckets != 65536) return hipErrorInvalidValue;
+  const dim3 grid(grid_for(count, kPlaceBlock * kPlaceIpt, 4096));
   const uint32_t mask = (uint32_t)nbuckets - 1;
-  if ((int64_t)P * nbuckets <= kPlaceLdsEntries)
-    hipLaunchKernelGGL(k_place<true>, grid, dim3(kPlaceBlock), 0, s, recv, A, m, shift, mask, P,
-                       rend, place_off);
+  if (nbuckets <= kPlaceLdsBuckets)
+    hipLaunchKernelGGL(k_place<true>, grid, dim3(kPlaceBlock), 0, s, src, out, k0, count, shift,
+                       mask, off_row);
   else
-    hipLaunchKernelGGL(k_place<false>, grid, dim3(kPlaceBlock), 0, s, recv, A, m, shift, mask, P,
-                       rend, place_off);
+    hipLaunchKernelGGL(k_place<false>, grid, dim3(kPlaceBlock), 0, s, src, out, k0, count, shift,
+                       mask, off_row);
   return hipGetLastError();
 }
 

@@ -14,11 +14,15 @@
 //      (replaces copyCountsToGlobalCounts + MPI_Exscan +
 //      copyStartsFromGlobalStarts, mpi/mpi_lsbsort.cpp:327-479: every rank
 //      scans the P x nbuckets matrix in digit-major, rank-minor order itself)
-//   3. host plan (lsb_plan_exchange): per-peer send/recv counts, placement table
+//   3. device plan (k_plan_*, same rule as lsb_plan_exchange): placement
+//      table on the device, the 2P send/recv counts to the host
 //   4. all-to-all-v of 16-byte records out of A into R (MPI_Alltoallv of
 //      24-byte ShuffleBufSortElement at mpi/mpi_lsbsort.cpp:563; no
-//      destination index travels: the receiver derives it from the counts)
-//   5. k_place: R -> B, swap (mpi/mpi_lsbsort.cpp:568-575)
+//      destination index travels: the receiver derives it from the counts),
+//      cut into `slices` groups: slice j carries part j of every peer segment
+//   5. k_place -> B on a second stream (mpi/mpi_lsbsort.cpp:568-575): the
+//      self segment straight out of A at once, slice j of R as soon as it has
+//      arrived, overlapping slice j+1 on the wire; then swap
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -49,6 +53,9 @@ struct Rank {
   int rank = 0;
   int dev = 0;
   hipStream_t stream = nullptr;
+  hipStream_t pstream = nullptr;        // placement stream (overlaps the exchange)
+  hipEvent_t pevent = nullptr;          // stream -> pstream handoff
+  hipEvent_t pdone = nullptr;           // pstream -> stream: placement finished
   int64_t here = 0;
   Elem* A = nullptr;  // per slots: input / output (DistributedArray A)
   Elem* B = nullptr;  // per slots: ping-pong partner
@@ -87,6 +94,7 @@ struct lsb_ctx {
   bool timing = false;
   bool force_exchange = false;
   bool skip_constant = true;  // lsb_sort skips digits on which all keys agree
+  int slices = 4;             // exchange slices (placement overlaps the next slice)
   // What the last lsb_sort ran (lsb_get_last_sort).
   int last_local_passes = 0;
   int last_exchanges = 0;
@@ -156,17 +164,19 @@ struct Timer {
   lsb_ctx* c;
   Rank* r;
   int kid;
+  hipStream_t stream;
   hipEvent_t start = nullptr;
-  Timer(lsb_ctx* c_, Rank* r_, int kid_) : c(c_), r(r_), kid(kid_) {
+  Timer(lsb_ctx* c_, Rank* r_, int kid_, hipStream_t s = nullptr)
+      : c(c_), r(r_), kid(kid_), stream(s ? s : r_->stream) {
     if (!c->timing) return;
     start = take_event(c);
-    if (start) (void)hipEventRecord(start, r->stream);
+    if (start) (void)hipEventRecord(start, stream);
   }
   void stop() {
     if (!start) return;
     hipEvent_t e = take_event(c);
     if (!e) return;
-    (void)hipEventRecord(e, r->stream);
+    (void)hipEventRecord(e, stream);
     c->pending.push_back({kid, r->dev, start, e});
     start = nullptr;
   }
@@ -220,6 +230,9 @@ int init_rank(lsb_ctx* c, Rank& r, int rank, int dev) {
   r.here = here_of(c->n, c->P, rank);
   HIP_TRY(hipSetDevice(dev));
   HIP_TRY(hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking));
+  HIP_TRY(hipStreamCreateWithFlags(&r.pstream, hipStreamNonBlocking));
+  HIP_TRY(hipEventCreateWithFlags(&r.pevent, hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&r.pdone, hipEventDisableTiming));
   const size_t per = (size_t)c->per;
   r.chunking = lsb::make_chunking(r.here, max_chunks_for_device(dev));
   const size_t hist_entries = (size_t)lsb::kBuckets * std::max(1, r.chunking.num_chunks);
@@ -274,6 +287,12 @@ void free_rank(Rank& r) {
   (void)hipFree(r.span_gather);
   (void)hipHostFree(r.span_h);
   (void)hipHostFree(r.counts_h);
+  if (r.pstream) {
+    (void)hipStreamSynchronize(r.pstream);
+    (void)hipStreamDestroy(r.pstream);
+  }
+  if (r.pevent) (void)hipEventDestroy(r.pevent);
+  if (r.pdone) (void)hipEventDestroy(r.pdone);
   if (r.stream) (void)hipStreamDestroy(r.stream);
   r = Rank();
 }
@@ -352,19 +371,60 @@ void plan_fetch(lsb_ctx* c, Rank& r) {
   }
 }
 
-// R -> B by the plan, then swap: A holds the pass result.
-int place_rank(lsb_ctx* c, Rank& r, int shift) {
-  {
-    Timer t(c, &r, LSB_K_PLACE);
-    HIP_TRY(hipSetDevice(r.dev));
-    const int64_t* rend = r.place + (size_t)c->P * c->nb;
-    HIP_TRY(lsb::launch_place(r.R, r.B, r.here, shift, c->nb, c->P, rend, r.place, r.stream));
+// ---- placement, overlapped with the exchange ------------------------------
+// Part j of n records cut into `slices` parts: [part(n, j), part(n, j + 1)).
+// Sender and receiver cut a segment alike (send_counts[q] at s equals
+// recv_counts[s] at q).
+int64_t part(int64_t n, int j, int slices) { return n * j / slices; }
+
+// Everything after this on r.stream waits for r.pstream's work so far.
+int join_place(Rank& r) {
+  HIP_TRY(hipEventRecord(r.pdone, r.pstream));
+  HIP_TRY(hipStreamWaitEvent(r.stream, r.pdone, 0));
+  return LSB_OK;
+}
+
+// Place one source's received range [k0, k0 + cnt) (records at src) into B.
+int place_range(lsb_ctx* c, Rank& r, int shift, int src_rank, const Elem* src, int64_t k0,
+                int64_t cnt) {
+  if (cnt <= 0) return LSB_OK;
+  Timer t(c, &r, LSB_K_PLACE, r.pstream);
+  HIP_TRY(lsb::launch_place(src, r.B, k0, cnt, shift, c->nb,
+                            r.place + (size_t)src_rank * c->nb, r.pstream));
+  return LSB_OK;
+}
+
+// The self segment needs no transfer: place it straight out of A as soon as
+// the plan is on the device (call after the host has the plan).
+int place_self(lsb_ctx* c, Rank& r, int shift) {
+  const int me = r.rank;
+  if (r.send_counts[me] != r.recv_counts[me])
+    return fail(LSB_ERR_STATE, "exchange", "self count mismatch");
+  HIP_TRY(hipSetDevice(r.dev));
+  HIP_TRY(hipEventRecord(r.pevent, r.stream));  // plan kernels done
+  HIP_TRY(hipStreamWaitEvent(r.pstream, r.pevent, 0));
+  return place_range(c, r, shift, me, r.A + r.send_displs[me], r.recv_displs[me],
+                     r.recv_counts[me]);
+}
+
+// Slice j of every peer segment has arrived in R (r.stream): place it on
+// r.pstream while r.stream carries slice j + 1.
+int place_slice(lsb_ctx* c, Rank& r, int shift, int j) {
+  HIP_TRY(hipSetDevice(r.dev));
+  HIP_TRY(hipEventRecord(r.pevent, r.stream));
+  HIP_TRY(hipStreamWaitEvent(r.pstream, r.pevent, 0));
+  for (int s = 0; s < c->P; ++s) {
+    if (s == r.rank) continue;
+    const int64_t lo = part(r.recv_counts[s], j, c->slices);
+    const int64_t hi = part(r.recv_counts[s], j + 1, c->slices);
+    LSB_TRY(place_range(c, r, shift, s, r.R + r.recv_displs[s] + lo, r.recv_displs[s] + lo, hi - lo));
   }
-  std::swap(r.A, r.B);
   return LSB_OK;
 }
 
 // ---- exchange: in-process loopback --------------------------------------
+// The same slices and placement as the RCCL path; device copies stand in for
+// ncclSend/ncclRecv.
 int exchange_loopback(lsb_ctx* c, int digit) {
   const int shift = digit * c->bits;
   const size_t nb = (size_t)c->nb;
@@ -388,26 +448,35 @@ int exchange_loopback(lsb_ctx* c, int digit) {
     HIP_TRY(hipStreamSynchronize(r.stream));
     plan_fetch(c, r);
   }
-  // all-to-all-v: segment q of rank s's digit-ordered A -> rank q's R.
-  for (Rank& q : c->ranks) {
-    Timer t(c, &q, LSB_K_EXCHANGE);
-    HIP_TRY(hipSetDevice(q.dev));
-    for (Rank& s : c->ranks) {
-      const int64_t cnt = s.send_counts[q.rank];
-      if (cnt != q.recv_counts[s.rank])
+  for (Rank& q : c->ranks)
+    for (Rank& s : c->ranks)
+      if (s.send_counts[q.rank] != q.recv_counts[s.rank])
         return fail(LSB_ERR_STATE, "exchange_loopback", "send/recv count mismatch");
-      if (cnt == 0) continue;
-      HIP_TRY(hipMemcpyAsync(q.R + q.recv_displs[s.rank], s.A + s.send_displs[q.rank],
-                             (size_t)cnt * sizeof(Elem), hipMemcpyDefault, q.stream));
+  for (Rank& r : c->ranks) LSB_TRY(place_self(c, r, shift));
+  // all-to-all-v, slice by slice: part j of segment q of rank s's
+  // digit-ordered A -> rank q's R.
+  for (int j = 0; j < c->slices; ++j) {
+    for (Rank& q : c->ranks) {
+      Timer t(c, &q, LSB_K_EXCHANGE);
+      HIP_TRY(hipSetDevice(q.dev));
+      for (Rank& s : c->ranks) {
+        if (s.rank == q.rank) continue;
+        const int64_t cnt = s.send_counts[q.rank];
+        const int64_t lo = part(cnt, j, c->slices), hi = part(cnt, j + 1, c->slices);
+        if (hi <= lo) continue;
+        HIP_TRY(hipMemcpyAsync(q.R + q.recv_displs[s.rank] + lo, s.A + s.send_displs[q.rank] + lo,
+                               (size_t)(hi - lo) * sizeof(Elem), hipMemcpyDefault, q.stream));
+      }
     }
+    for (Rank& q : c->ranks) LSB_TRY(place_slice(c, q, shift, j));
   }
-  // Every rank's copies must be done before any rank's placement reuses B/A
-  // (placement writes B, the next pass rewrites the A that was copied from).
+  // Every rank's copies out of A must be done before any rank's next pass
+  // rewrites that A (it becomes B after the swap).
   for (Rank& r : c->ranks) {
-    HIP_TRY(hipSetDevice(r.dev));
+    LSB_TRY(join_place(r));
     HIP_TRY(hipStreamSynchronize(r.stream));
+    std::swap(r.A, r.B);
   }
-  for (Rank& r : c->ranks) LSB_TRY(place_rank(c, r, shift));
   return LSB_OK;
 }
 
@@ -427,29 +496,32 @@ int exchange_rccl(lsb_ctx* c, int digit) {
   LSB_TRY(plan_launch(c, r));
   HIP_TRY(hipStreamSynchronize(r.stream));
   plan_fetch(c, r);
-  {
-    Timer t(c, &r, LSB_K_EXCHANGE);
-    const int me = r.rank;
-    // The self segment is a device copy; the P-1 peers go over RCCL.
-    if (r.send_counts[me] != r.recv_counts[me])
-      return fail(LSB_ERR_STATE, "exchange_rccl", "self count mismatch");
-    if (r.send_counts[me] > 0)
-      HIP_TRY(hipMemcpyAsync(r.R + r.recv_displs[me], r.A + r.send_displs[me],
-                             (size_t)r.send_counts[me] * sizeof(Elem), hipMemcpyDeviceToDevice,
-                             r.stream));
-    RCCL_TRY(ncclGroupStart());
-    for (int q = 0; q < P; ++q) {
-      if (q == me) continue;
-      if (r.send_counts[q] > 0)
-        RCCL_TRY(ncclSend(r.A + r.send_displs[q], (size_t)r.send_counts[q] * 2, ncclUint64, q,
-                          c->comm, r.stream));
-      if (r.recv_counts[q] > 0)
-        RCCL_TRY(ncclRecv(r.R + r.recv_displs[q], (size_t)r.recv_counts[q] * 2, ncclUint64, q,
-                          c->comm, r.stream));
+  LSB_TRY(place_self(c, r, shift));
+  const int me = r.rank;
+  for (int j = 0; j < c->slices; ++j) {
+    {
+      Timer t(c, &r, LSB_K_EXCHANGE);
+      RCCL_TRY(ncclGroupStart());
+      for (int q = 0; q < P; ++q) {
+        if (q == me) continue;
+        const int64_t slo = part(r.send_counts[q], j, c->slices);
+        const int64_t shi = part(r.send_counts[q], j + 1, c->slices);
+        const int64_t rlo = part(r.recv_counts[q], j, c->slices);
+        const int64_t rhi = part(r.recv_counts[q], j + 1, c->slices);
+        if (shi > slo)
+          RCCL_TRY(ncclSend(r.A + r.send_displs[q] + slo, (size_t)(shi - slo) * 2, ncclUint64, q,
+                            c->comm, r.stream));
+        if (rhi > rlo)
+          RCCL_TRY(ncclRecv(r.R + r.recv_displs[q] + rlo, (size_t)(rhi - rlo) * 2, ncclUint64, q,
+                            c->comm, r.stream));
+      }
+      RCCL_TRY(ncclGroupEnd());
     }
-    RCCL_TRY(ncclGroupEnd());
+    LSB_TRY(place_slice(c, r, shift, j));
   }
-  return place_rank(c, r, shift);
+  LSB_TRY(join_place(r));
+  std::swap(r.A, r.B);
+  return LSB_OK;
 }
 
 // One exchange digit: its 8-bit local sub-passes, then (P > 1) the exchange.
@@ -680,6 +752,11 @@ int lsb_set_option(lsb_ctx_t* c, int option, int64_t value) {
       return LSB_OK;
     case LSB_OPT_SKIP_CONSTANT_DIGITS:
       c->skip_constant = value != 0;
+      return LSB_OK;
+    case LSB_OPT_EXCHANGE_SLICES:
+      if (value < 1 || value > 64)
+        return fail(LSB_ERR_INVALID, "lsb_set_option", "exchange slices must be 1..64");
+      c->slices = (int)value;
       return LSB_OK;
     default:
       return fail(LSB_ERR_INVALID, "lsb_set_option", "unknown option");

@@ -254,6 +254,30 @@ def test_forced_exchange_at_p1(lsb_built, oracle_mod, digests):
         assert oracle_mod.digest(w.gather_global()) == d["output"]
 
 
+@pytest.mark.parametrize("slices", [1, 3, 7])
+@pytest.mark.parametrize("n,P,bits", [(100_003, 2, 8), (100_003, 5, 16), (250_001, 8, 8),
+                                      (9, 8, 16), (13, 3, 8)])
+def test_exchange_slices(lsb_built, oracle_mod, slices, n, P, bits):
+    """The all-to-all cut into slices, each placed while the next is in flight."""
+    rng = np.random.default_rng(n + 7 * P + slices)
+    a = np.zeros(n, dtype=DT)
+    a["key"] = rng.integers(0, 2**64 - 1, n, dtype=np.uint64)
+    a["key"][rng.random(n) < 0.3] = np.uint64(0x1234)  # heavy duplicates: uneven segments
+    a["val"] = np.arange(n, dtype=np.uint64)
+    with lsb_built.World(n, ranks=P, radix_bits=bits) as w:
+        w.set_option(lsb_built.OPT_EXCHANGE_SLICES, slices)
+        w.scatter_global(a)
+        w.my_sort()
+        assert np.array_equal(w.gather_global(), oracle_mod.stable_sort(a))
+
+
+def test_exchange_slices_option_range(lsb_built):
+    with lsb_built.World(10, ranks=2) as w:
+        for bad in (0, 65):
+            with pytest.raises(lsb_built.LsbError):
+                w.set_option(lsb_built.OPT_EXCHANGE_SLICES, bad)
+
+
 def test_rccl_world_of_one(lsb_built, oracle_mod, digests):
     d = next(r for r in digests["rows"] if r["P"] == 1)
     uid = lsb_built.get_unique_id()
