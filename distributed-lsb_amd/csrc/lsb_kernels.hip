@@ -78,16 +78,22 @@ __device__ __forceinline__ uint32_t mbcnt(uint64_t mask) {
                                    __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
-// Lanes of `active` whose 8-bit digit equals mine.
+// Lanes of `active` whose 8-bit digit equals mine.  Per bit: t = my bit
+// sign-extended (0 or ~0), bal = lanes with the bit set, and the lanes whose
+// bit equals mine are ~(bal ^ t); one gfx950 v_bitop3 per 32-bit half folds
+// that into the running mask (truth table 0x90 = a & ~(b ^ c), index
+// a*4 + b*2 + c).  4 VALU per bit; the select form (set ? bal : ~bal)
+// compiles to 9.
 __device__ __forceinline__ uint64_t match_digit8(uint32_t d, uint64_t active) {
-  uint64_t m = active;
+  uint32_t lo = (uint32_t)active, hi = (uint32_t)(active >> 32);
 #pragma unroll
   for (int bit = 0; bit < 8; ++bit) {
-    const bool set = (d >> bit) & 1u;
-    const uint64_t bal = __ballot(set);
-    m &= set ? bal : ~bal;
+    const uint32_t t = (uint32_t)__builtin_amdgcn_sbfe((int)d, bit, 1);
+    const uint64_t bal = __ballot(t != 0u);
+    lo = __builtin_amdgcn_bitop3_b32(lo, (uint32_t)bal, t, 0x90);
+    hi = __builtin_amdgcn_bitop3_b32(hi, (uint32_t)(bal >> 32), t, 0x90);
   }
-  return m;
+  return ((uint64_t)hi << 32) | lo;
 }
 
 __device__ __forceinline__ Elem load_elem(const Elem* p) {
