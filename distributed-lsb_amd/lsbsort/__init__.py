@@ -31,7 +31,8 @@ import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 ROOT_DIR = os.path.dirname(PKG_DIR)
-LIB_PATH = os.path.join(ROOT_DIR, "build", "liblsb.so")
+# LSB_LIBRARY: another build of the same ABI (A/B timing of kernel variants).
+LIB_PATH = os.environ.get("LSB_LIBRARY") or os.path.join(ROOT_DIR, "build", "liblsb.so")
 HARNESS_PATH = os.path.join(ROOT_DIR, "build", "hip_lsbsort")
 HEADER_PATH = os.path.join(os.path.dirname(ROOT_DIR), "include", "lsb.h")
 
