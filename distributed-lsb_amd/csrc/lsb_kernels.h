@@ -64,8 +64,17 @@ hipError_t launch_scan(const uint32_t* chunk_hist, int G, uint64_t* chunk_off,
 // Stable counting-sort scatter of one digit: out[pos] with
 // pos = bucket_start[b] + chunk_off[b][c] + rank of the element among the
 // chunk's digit-b elements (localShuffle, mpi/mpi_lsbsort.cpp:240-246).
+// first16 (optional; the high byte of a 16-bit digit whose low byte the input
+// is sorted by): atomicMin of candidate start positions of every 16-bit digit
+// at shift - 8; reset it with launch_starts_reset, then launch_starts_to_counts.
 hipError_t launch_scatter(const Elem* in, Elem* out, int64_t m, int shift, Chunking ch,
-                          const uint64_t* chunk_off, const uint64_t* totals, hipStream_t s);
+                          const uint64_t* chunk_off, const uint64_t* totals, int64_t* first16,
+                          hipStream_t s);
+hipError_t launch_starts_reset(int64_t* first16, hipStream_t s);
+// counts[d] of a rank whose m records are sorted by the 16-bit digit, from the
+// first index of every present digit (first[d] < 0 or >= m: absent).
+hipError_t launch_starts_to_counts(const int64_t* first16, int64_t m, uint64_t* counts,
+                                   hipStream_t s);
 
 // Receiver-side placement of one source's received range: src[i] (receive
 // index k0 + i) goes to out[off_row[digit] + k0 + i], off_row = the source's

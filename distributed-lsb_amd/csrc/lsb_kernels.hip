@@ -318,12 +318,27 @@ __global__ __launch_bounds__(kScanBlock) void k_scan(const uint32_t* __restrict_
 // last line per bucket can still be partial.
 constexpr int kLineElems = 8;  // 128-B line / 16-B record
 
-template <int BLOCK, int IPT>
+// STARTS (P > 1, high byte of a 16-bit exchange digit): the output is then
+// sorted by the 16-bit digit at shift16 = shift - 8, and the exchange needs
+// its 65536 counts.  Instead of re-reading the output (k_digit_starts), the
+// scatter marks where a 16-bit digit may begin: a record whose predecessor
+// in the output has a different low byte, or is unknown.  A workgroup's
+// bucket-b records land contiguously in stream order, so the predecessor is
+// the previous record of the tile's run, the last record of this
+// workgroup's previous run in b (prevlo[b]), or another workgroup's
+// (unknown: the chunk's first record in b).  atomicMin over the marks is the
+// first position of every digit: every true start is marked, and every other
+// mark lies after it.  The input is sorted by the low byte, so a tile whose
+// first and last records share it has one low byte throughout: only each
+// run's first record needs a look (by its bucket's thread, once per tile).
+// The rare tile across a low-byte boundary walks its runs.
+template <int BLOCK, int IPT, bool STARTS>
 __global__ __launch_bounds__(BLOCK, 2) void k_scatter(const Elem* __restrict__ in,
                                                       Elem* __restrict__ out, int64_t m,
                                                       int shift, int64_t chunk_elems, int G,
                                                       const uint64_t* __restrict__ chunk_off,
-                                                      const uint64_t* __restrict__ totals) {
+                                                      const uint64_t* __restrict__ totals,
+                                                      long long* __restrict__ first16) {
   constexpr int W = BLOCK / 64;
   constexpr int T = BLOCK * IPT;
   constexpr int CY = kLineElems - 1;
@@ -335,6 +350,8 @@ __global__ __launch_bounds__(BLOCK, 2) void k_scatter(const Elem* __restrict__ i
   __shared__ int64_t lim[kBuckets];         // write only dest < lim[digit] (E_b)
   __shared__ uint64_t scan64[W];
   __shared__ uint32_t scan32[W];
+  __shared__ int32_t prevlo[STARTS ? kBuckets : 1];  // low byte of b's last record, -1 = none
+  __shared__ uint32_t tile_lo[2];                     // low byte of the tile's first, last record
 
   const int t = threadIdx.x;
   const int w = t >> 6;
@@ -342,6 +359,8 @@ __global__ __launch_bounds__(BLOCK, 2) void k_scatter(const Elem* __restrict__ i
   const int c = blockIdx.x;
   const int64_t beg = (int64_t)c * chunk_elems;
   const int64_t end = beg + chunk_elems < m ? beg + chunk_elems : m;
+  const int shift16 = shift - 8;
+  if (STARTS && t < kBuckets) prevlo[t] = -1;
 
   // Global start of this chunk's run of each bucket.
   uint64_t run = 0;
@@ -382,6 +401,8 @@ __global__ __launch_bounds__(BLOCK, 2) void k_scatter(const Elem* __restrict__ i
       const uint32_t below = mbcnt(mt);
       const uint32_t pre = wcnt[w][d];
       rk[i] = pre + below;
+      if (STARTS && (wbase + i * 64 == 0 || wbase + i * 64 == nvalid - 1))
+        tile_lo[wbase + i * 64 == 0 ? 0 : 1] = (uint32_t)(e[i].key >> shift16) & 0xFFu;
       if (valid && below == 0) wcnt[w][d] = pre + (uint32_t)__popcll(mt);
     }
     __syncthreads();
@@ -398,6 +419,9 @@ __global__ __launch_bounds__(BLOCK, 2) void k_scatter(const Elem* __restrict__ i
     }
     uint32_t tile_total;
     const uint32_t lstart = block_exclusive_scan<BLOCK>(cnt, scan32, &tile_total);
+    // Read now: the next tile rewrites tile_lo before its first barrier.
+    const uint32_t tlo0 = STARTS ? tile_lo[0] : 0u;
+    const bool tmixed = STARTS && tile_lo[0] != tile_lo[1];
     // Run of bucket t in this tile: dest [R, R + cnt); carried [A, R).
     // Write [A, E): E = end of the last whole line, or everything at the
     // chunk's last tile; E == A means the line is still incomplete.
@@ -452,6 +476,23 @@ __global__ __launch_bounds__(BLOCK, 2) void k_scatter(const Elem* __restrict__ i
         if ((uint32_t)i >= keep && (uint32_t)i < new_len) cy[i] = stage[src0 + (i - (int)keep)];
       }
       cy_len = new_len;
+      if (STARTS && cnt > 0) {
+        // Run of bucket t in this tile: stage [lstart, lstart + cnt) -> out [R, ...).
+        uint32_t lo = (uint32_t)(stage[lstart].key >> shift16) & 0xFFu;
+        if (prevlo[t] != (int32_t)lo)
+          atomicMin(&first16[(stage[lstart].key >> shift16) & 0xFFFFu], (long long)R);
+        if (tmixed) {  // the tile straddles a low-byte boundary
+          for (uint32_t k = 1; k < cnt; ++k) {
+            const uint64_t key = stage[lstart + k].key;
+            const uint32_t l = (uint32_t)(key >> shift16) & 0xFFu;
+            if (l != lo) atomicMin(&first16[(key >> shift16) & 0xFFFFu], (long long)(R + k));
+            lo = l;
+          }
+        } else {
+          lo = tlo0;
+        }
+        prevlo[t] = (int32_t)lo;
+      }
     }
   }
 }
@@ -541,7 +582,7 @@ __global__ __launch_bounds__(kStartsBlock) void k_starts_to_counts(const int64_t
   int64_t mine = m;
   for (int j = kStartsPer - 1; j >= 0; --j) {
     const int64_t f = first[d0 + j];
-    if (f >= 0) mine = f;
+    if (f >= 0 && f < m) mine = f;
   }
   // suffix min over threads t+1.. (starts increase with the digit, so the
   // next present start after my range is the first present start of the
@@ -566,7 +607,7 @@ __global__ __launch_bounds__(kStartsBlock) void k_starts_to_counts(const int64_t
   int64_t next = after;
   for (int j = kStartsPer - 1; j >= 0; --j) {
     const int64_t f = first[d0 + j];
-    if (f >= 0) {
+    if (f >= 0 && f < m) {
       counts[d0 + j] = (uint64_t)(next - f);
       next = f;
     } else {
@@ -767,6 +808,17 @@ hipError_t launch_digit16_counts(const Elem* A, int64_t m, int shift, int64_t* f
   return hipGetLastError();
 }
 
+hipError_t launch_starts_reset(int64_t* first, hipStream_t s) {
+  // 0x7f7f... > any record index: "absent" for atomicMin and for the counts.
+  return hipMemsetAsync(first, 0x7f, sizeof(int64_t) * 65536, s);
+}
+
+hipError_t launch_starts_to_counts(const int64_t* first, int64_t m, uint64_t* counts,
+                                   hipStream_t s) {
+  hipLaunchKernelGGL(k_starts_to_counts, dim3(1), dim3(kStartsBlock), 0, s, first, m, counts);
+  return hipGetLastError();
+}
+
 hipError_t launch_upsweep(const Elem* A, int64_t m, int shift, Chunking ch, uint32_t* chunk_hist,
                           uint64_t* span, hipStream_t s) {
   if (m <= 0) return hipSuccess;
@@ -790,11 +842,19 @@ hipError_t launch_scan(const uint32_t* chunk_hist, int G, uint64_t* chunk_off, u
 }
 
 hipError_t launch_scatter(const Elem* in, Elem* out, int64_t m, int shift, Chunking ch,
-                          const uint64_t* chunk_off, const uint64_t* totals, hipStream_t s) {
+                          const uint64_t* chunk_off, const uint64_t* totals, int64_t* first16,
+                          hipStream_t s) {
   if (m <= 0) return hipSuccess;
-  hipLaunchKernelGGL((k_scatter<kScatterBlock, kScatterIpt>), dim3(ch.num_chunks),
-                     dim3(kScatterBlock), 0, s, in, out, m, shift, ch.chunk_elems, ch.num_chunks,
-                     chunk_off, totals);
+  if (first16) {
+    if (shift < 8) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((k_scatter<kScatterBlock, kScatterIpt, true>), dim3(ch.num_chunks),
+                       dim3(kScatterBlock), 0, s, in, out, m, shift, ch.chunk_elems, ch.num_chunks,
+                       chunk_off, totals, reinterpret_cast<long long*>(first16));
+  } else {
+    hipLaunchKernelGGL((k_scatter<kScatterBlock, kScatterIpt, false>), dim3(ch.num_chunks),
+                       dim3(kScatterBlock), 0, s, in, out, m, shift, ch.chunk_elems, ch.num_chunks,
+                       chunk_off, totals, nullptr);
+  }
   return hipGetLastError();
 }
 

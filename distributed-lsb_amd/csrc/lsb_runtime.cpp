@@ -65,6 +65,7 @@ struct Rank {
   uint64_t* totals = nullptr;           // [256] local counts of the current 8-bit digit
   uint64_t* totals16 = nullptr;         // [65536] local counts of a 16-bit digit (bits = 16, P > 1)
   int64_t* first16 = nullptr;           // [65536] scratch of the 16-bit count
+  bool starts_fused = false;            // first16 holds this digit's starts (marked by k_scatter)
   uint64_t* gather = nullptr;           // [P][nb] all-gathered counts
   int64_t* place = nullptr;             // [P][nb] place_off, then [P] rend (device plan)
   int64_t* plan_work = nullptr;         // [P][nb] device-plan scratch
@@ -304,12 +305,17 @@ Rank* local_rank(lsb_ctx* c, int rank) {
 }
 
 // ---- one local stable 8-bit pass A -> B, then swap (localShuffle) -------
-int local_pass(lsb_ctx* c, Rank& r, int shift, bool want_span = false) {
+// want_span: also reduce the key span (lsb_sort's first pass).  starts16:
+// this is the high byte of a 16-bit exchange digit; the scatter also marks
+// the digit's run starts, so digit_counts needs no extra read.
+int local_pass(lsb_ctx* c, Rank& r, int shift, bool want_span = false, bool starts16 = false) {
   HIP_TRY(hipSetDevice(r.dev));
+  r.starts_fused = starts16;
   if (r.here == 0) {
     HIP_TRY(hipMemsetAsync(r.totals, 0, sizeof(uint64_t) * lsb::kBuckets, r.stream));
     return LSB_OK;
   }
+  if (starts16) HIP_TRY(lsb::launch_starts_reset(r.first16, r.stream));
   const lsb::Chunking& ch = r.chunking;
   {
     Timer t(c, &r, LSB_K_UPSWEEP);
@@ -322,7 +328,8 @@ int local_pass(lsb_ctx* c, Rank& r, int shift, bool want_span = false) {
   }
   {
     Timer t(c, &r, LSB_K_SCATTER);
-    HIP_TRY(lsb::launch_scatter(r.A, r.B, r.here, shift, ch, r.chunk_off, r.totals, r.stream));
+    HIP_TRY(lsb::launch_scatter(r.A, r.B, r.here, shift, ch, r.chunk_off, r.totals,
+                                starts16 ? r.first16 : nullptr, r.stream));
     if (c->timing) c->scatter_elems += r.here;
   }
   std::swap(r.A, r.B);
@@ -338,7 +345,11 @@ int digit_counts(lsb_ctx* c, Rank& r, int digit, const uint64_t** counts) {
   HIP_TRY(hipSetDevice(r.dev));
   {
     Timer t(c, &r, LSB_K_UPSWEEP);
-    HIP_TRY(lsb::launch_digit16_counts(r.A, r.here, digit * 16, r.first16, r.totals16, r.stream));
+    if (r.starts_fused)  // the high-byte scatter marked the starts
+      HIP_TRY(lsb::launch_starts_to_counts(r.first16, r.here, r.totals16, r.stream));
+    else  // high byte constant (skipped) or lsb_pass: read A once more
+      HIP_TRY(lsb::launch_digit16_counts(r.A, r.here, digit * 16, r.first16, r.totals16,
+                                         r.stream));
   }
   *counts = r.totals16;
   return LSB_OK;
@@ -529,10 +540,14 @@ int exchange_rccl(lsb_ctx* c, int digit) {
 // is the identity and is skipped (all ~0 = run everything).  want_span: the
 // first sub-pass also reduces the key span (lsb_sort, digit 0).
 int do_pass(lsb_ctx* c, int digit, uint64_t varying = ~0ull, bool want_span = false) {
-  for (int sub = 0; sub < c->bits / lsb::kDigitBits; ++sub) {
+  for (Rank& r : c->ranks) r.starts_fused = false;
+  const int subs = c->bits / lsb::kDigitBits;
+  for (int sub = 0; sub < subs; ++sub) {
     const int shift = digit * c->bits + sub * lsb::kDigitBits;
     if (!want_span && ((varying >> shift) & (lsb::kBuckets - 1)) == 0) continue;
-    for (Rank& r : c->ranks) LSB_TRY(local_pass(c, r, shift, want_span && sub == 0));
+    // The high byte of a 16-bit exchange digit also marks the digit's starts.
+    const bool starts16 = exchanging(c) && subs == 2 && sub == 1;
+    for (Rank& r : c->ranks) LSB_TRY(local_pass(c, r, shift, want_span && sub == 0, starts16));
     ++c->last_local_passes;
   }
   if (!exchanging(c)) return LSB_OK;

@@ -228,7 +228,7 @@ int main(int argc, char** argv) {
     KFn k0 = k_scatter_v<256, 16, false, false, 2>;
     float t = time_ms([&] { hipLaunchKernelGGL(k0, dim3(ch.num_chunks), dim3(256), 0, 0, b.in, b.ref, m, shift, ch.chunk_elems, ch.num_chunks, b.off, b.tot); }, reps);
     printf("no-carry k_scatter_v       %8.3f ms  %7.1f GB/s\n", t, gb / t * 1e3);
-    float tp = time_ms([&] { CK(launch_scatter(b.in, b.out, m, shift, ch, b.off, b.tot, 0)); }, reps);
+    float tp = time_ms([&] { CK(launch_scatter(b.in, b.out, m, shift, ch, b.off, b.tot, nullptr, 0)); }, reps);
     CK(hipMemset(bad, 0, sizeof(unsigned long long)));
     hipLaunchKernelGGL(k_diff, dim3(4096), dim3(256), 0, 0, b.out, b.ref, m, bad);
     unsigned long long h = 0;
@@ -260,11 +260,6 @@ int main(int argc, char** argv) {
     fflush(stdout);
   };
 
-  run_variant("carry 256x16 G512", 512, k_scatter<256, 16>, 256, 4096, true);
-  run_variant("carry 1024x8 G256", 256, k_scatter<1024, 8>, 1024, 8192, true);
-  run_variant("carry 512x16 G256", 256, k_scatter<512, 16>, 512, 8192, true);
-  run_variant("carry 512x8 G512", 512, k_scatter<512, 8>, 512, 4096, true);
-  run_variant("carry 256x8 G1024", 1024, k_scatter<256, 8>, 256, 2048, true);
   run_variant("v256x16 pf SEQ", 512, k_scatter_v<256, 16, true, true, 2>, 256, 4096, false);
   {
     float ms = time_ms([&] { hipLaunchKernelGGL((k_copy8<256, 8>), dim3((unsigned)(m / 2048)), dim3(256), 0, 0, b.in, b.out, m); }, reps);

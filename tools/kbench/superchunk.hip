@@ -54,7 +54,7 @@ int main() {
   auto one = [&] {
     CK(launch_upsweep(in, m, shift, ch, hist, nullptr, 0));
     CK(launch_scan(hist, ch.num_chunks, off, tot, 0));
-    CK(launch_scatter(in, ref, m, shift, ch, off, tot, 0));
+    CK(launch_scatter(in, ref, m, shift, ch, off, tot, nullptr, 0));
   };
   float t1 = time_ms(one, 5);
   printf("one-shot pass                 %7.3f ms\n", t1);
@@ -68,7 +68,7 @@ int main() {
           CK(launch_upsweep(in + s0, sc, shift, cs, hist, nullptr, 0));
           CK(launch_scan(hist, cs.num_chunks, off, tot, 0));
           hipLaunchKernelGGL(k_add_base, dim3(1), dim3(256), 0, 0, off, cs.num_chunks, base, tot);
-          CK(launch_scatter(in + s0, out, sc, shift, cs, off, zero, 0));
+          CK(launch_scatter(in + s0, out, sc, shift, cs, off, zero, nullptr, 0));
         }
       };
       float t = time_ms(pass, 3);
