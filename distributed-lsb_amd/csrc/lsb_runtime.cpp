@@ -96,6 +96,7 @@ struct lsb_ctx {
   bool force_exchange = false;
   bool skip_constant = true;  // lsb_sort skips digits on which all keys agree
   int slices = 4;             // exchange slices (placement overlaps the next slice)
+  bool p2p = false;           // RCCL exchange as grouped ncclSend/ncclRecv, not ncclAllToAllv
   // What the last lsb_sort ran (lsb_get_last_sort).
   int last_local_passes = 0;
   int last_exchanges = 0;
@@ -435,7 +436,7 @@ int place_slice(lsb_ctx* c, Rank& r, int shift, int j) {
 
 // ---- exchange: in-process loopback --------------------------------------
 // The same slices and placement as the RCCL path; device copies stand in for
-// ncclSend/ncclRecv.
+// ncclAllToAllv.
 int exchange_loopback(lsb_ctx* c, int digit) {
   const int shift = digit * c->bits;
   const size_t nb = (size_t)c->nb;
@@ -509,24 +510,34 @@ int exchange_rccl(lsb_ctx* c, int digit) {
   plan_fetch(c, r);
   LSB_TRY(place_self(c, r, shift));
   const int me = r.rank;
+  // ncclAllToAllv per slice (the reference's MPI_Alltoallv,
+  // mpi/mpi_lsbsort.cpp:316-324), in uint64 units; the self entry is 0
+  // because the self segment was placed straight out of A.
+  std::vector<size_t> sc(P), sd(P), rc(P), rdp(P);
   for (int j = 0; j < c->slices; ++j) {
     {
       Timer t(c, &r, LSB_K_EXCHANGE);
-      RCCL_TRY(ncclGroupStart());
       for (int q = 0; q < P; ++q) {
-        if (q == me) continue;
         const int64_t slo = part(r.send_counts[q], j, c->slices);
         const int64_t shi = part(r.send_counts[q], j + 1, c->slices);
         const int64_t rlo = part(r.recv_counts[q], j, c->slices);
         const int64_t rhi = part(r.recv_counts[q], j + 1, c->slices);
-        if (shi > slo)
-          RCCL_TRY(ncclSend(r.A + r.send_displs[q] + slo, (size_t)(shi - slo) * 2, ncclUint64, q,
-                            c->comm, r.stream));
-        if (rhi > rlo)
-          RCCL_TRY(ncclRecv(r.R + r.recv_displs[q] + rlo, (size_t)(rhi - rlo) * 2, ncclUint64, q,
-                            c->comm, r.stream));
+        sc[q] = q == me ? 0 : (size_t)(shi - slo) * 2;
+        rc[q] = q == me ? 0 : (size_t)(rhi - rlo) * 2;
+        sd[q] = (size_t)(r.send_displs[q] + slo) * 2;
+        rdp[q] = (size_t)(r.recv_displs[q] + rlo) * 2;
       }
-      RCCL_TRY(ncclGroupEnd());
+      if (!c->p2p) {
+        RCCL_TRY(ncclAllToAllv(r.A, sc.data(), sd.data(), r.R, rc.data(), rdp.data(), ncclUint64,
+                               c->comm, r.stream));
+      } else {  // the same exchange as explicit grouped point-to-point calls
+        RCCL_TRY(ncclGroupStart());
+        for (int q = 0; q < P; ++q) {
+          if (sc[q] > 0) RCCL_TRY(ncclSend(r.A + sd[q] / 2, sc[q], ncclUint64, q, c->comm, r.stream));
+          if (rc[q] > 0) RCCL_TRY(ncclRecv(r.R + rdp[q] / 2, rc[q], ncclUint64, q, c->comm, r.stream));
+        }
+        RCCL_TRY(ncclGroupEnd());
+      }
     }
     LSB_TRY(place_slice(c, r, shift, j));
   }
@@ -767,6 +778,9 @@ int lsb_set_option(lsb_ctx_t* c, int option, int64_t value) {
       return LSB_OK;
     case LSB_OPT_SKIP_CONSTANT_DIGITS:
       c->skip_constant = value != 0;
+      return LSB_OK;
+    case LSB_OPT_EXCHANGE_P2P:
+      c->p2p = value != 0;
       return LSB_OK;
     case LSB_OPT_EXCHANGE_SLICES:
       if (value < 1 || value > 64)

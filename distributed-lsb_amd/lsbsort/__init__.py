@@ -44,7 +44,7 @@ LSB_ERR_VERIFY = 5
 DIST_UNIFORM, DIST_ZIPF = 0, 1
 K_UPSWEEP, K_SCAN, K_SCATTER, K_EXCHANGE, K_PLACE, K_SORT = range(6)
 KERNEL_NAMES = ("upsweep", "scan", "scatter", "exchange", "place", "sort")
-OPT_TIMING, OPT_FORCE_EXCHANGE, OPT_SKIP_CONSTANT_DIGITS, OPT_EXCHANGE_SLICES = 0, 1, 2, 3
+OPT_TIMING, OPT_FORCE_EXCHANGE, OPT_SKIP_CONSTANT_DIGITS, OPT_EXCHANGE_SLICES, OPT_EXCHANGE_P2P = 0, 1, 2, 3, 4
 
 
 class LsbError(RuntimeError):

@@ -21,7 +21,7 @@
  *                        with exactly the all-to-all-v semantics of RCCL.
  *   - lsb_create_rank(): one process per GPU (torchrun / hip_lsbsort --gpus);
  *                        this process is rank `rank`; the exchange is RCCL
- *                        (AllGather of bucket counts + grouped Send/Recv)
+ *                        (AllGather of bucket counts + AllToAllv)
  *                        over xGMI.  Collective calls must be made by all
  *                        ranks in the same order, as in the MPI reference.
  * The context owns every device buffer (A, B, send/recv, histograms, RCCL
@@ -74,6 +74,8 @@ typedef struct lsb_ctx lsb_ctx_t;
 #define LSB_OPT_EXCHANGE_SLICES 3  /* 1..64 (default 4): the all-to-all of a pass is cut into
                                       this many groups; each slice is placed while the next
                                       is in flight */
+#define LSB_OPT_EXCHANGE_P2P    4  /* RCCL contexts: 0 (default) ncclAllToAllv per slice,
+                                      1 the same as grouped ncclSend/ncclRecv */
 
 /* ---- geometry: DistributedArray::create (mpi/mpi_lsbsort.cpp:144-149) ---- */
 int64_t lsb_per_rank(int64_t n_total, int num_ranks);            /* ceil(n/P) */

@@ -278,12 +278,15 @@ def test_exchange_slices_option_range(lsb_built):
                 w.set_option(lsb_built.OPT_EXCHANGE_SLICES, bad)
 
 
-def test_rccl_world_of_one(lsb_built, oracle_mod, digests):
+@pytest.mark.parametrize("p2p", [0, 1])
+def test_rccl_world_of_one(lsb_built, oracle_mod, digests, p2p):
+    """ncclAllToAllv (default) and grouped ncclSend/ncclRecv."""
     d = next(r for r in digests["rows"] if r["P"] == 1)
     uid = lsb_built.get_unique_id()
     w = lsb_built.World.rank(d["n"], 1, 0, 0, uid)
     try:
         w.set_option(lsb_built.OPT_FORCE_EXCHANGE, 1)
+        w.set_option(lsb_built.OPT_EXCHANGE_P2P, p2p)
         w.generate()
         w.barrier()
         w.my_sort()
