@@ -182,3 +182,50 @@ def simulate16(lsbsort, oracle, n, P):
 def test_simulated_exchange_radix16(lsb_built, oracle_mod, n, P):
     out = simulate16(lsb_built, oracle_mod, n, P)
     assert np.array_equal(out, oracle_mod.mpi_sort(n, P))
+
+
+# ------------------------------------------------------------ error paths
+# Checks that return before any device call, so they run without a GPU.
+def test_error_codes_without_device(lsb_built):
+    import ctypes
+    lib = lsb_built._lib()
+    ctx = ctypes.c_void_p()
+    # lsb_create: null out, bad P, bad n, unsupported radix
+    assert lib.lsb_create(None, 10, 1, None, 8) == 1
+    assert lib.lsb_create(ctypes.byref(ctx), 10, 0, None, 8) == 1
+    assert lib.lsb_create(ctypes.byref(ctx), 10, 65, None, 8) == 1
+    assert lib.lsb_create(ctypes.byref(ctx), -1, 1, None, 8) == 1
+    assert lib.lsb_create(ctypes.byref(ctx), 10, 1, None, 12) == 6
+    assert not ctx.value
+    uid = bytes(128)
+    assert lib.lsb_create_rank(ctypes.byref(ctx), 10, 2, 2, 0, 8, uid) == 1   # rank >= P
+    assert lib.lsb_create_rank(ctypes.byref(ctx), 10, 2, 0, 0, 8, None) == 1  # no id
+    assert lib.lsb_create_rank(ctypes.byref(ctx), 10, 2, 0, 0, 32, uid) == 6
+    # every context call rejects a null context
+    n = ctypes.c_int64()
+    assert lib.lsb_sort(None) == 1
+    assert lib.lsb_pass(None, 0) == 1
+    assert lib.lsb_sync(None) == 1
+    assert lib.lsb_generate(None) == 1
+    assert lib.lsb_set_option(None, 0, 1) == 1
+    assert lib.lsb_verify(None, ctypes.byref(n)) == 1
+    assert lib.lsb_get_kernel_stats(None, 0, None, None) == 1
+    assert lib.lsb_get_last_sort(None, None, None, None) == 1
+    lib.lsb_destroy(None)  # no-op
+    for code in range(8):
+        assert lib.lsb_strerror(code)
+
+
+def test_planner_rejects_bad_input(lsb_built):
+    import ctypes
+    lib = lsb_built._lib()
+    P, nb = 2, 256
+    hist = np.zeros((P, nb), dtype=np.int64)
+    outs = [np.zeros(P, dtype=np.int64) for _ in range(4)] + [np.zeros(P * nb, dtype=np.int64)]
+    ptrs = [o.ctypes.data for o in outs]
+    assert lib.lsb_plan_exchange(0, P, 0, nb, hist.ctypes.data, *ptrs) == 0
+    assert lib.lsb_plan_exchange(0, P, 2, nb, hist.ctypes.data, *ptrs) == 1    # rank >= P
+    hist[0, 3] = -1
+    assert lib.lsb_plan_exchange(10, P, 0, nb, hist.ctypes.data, *ptrs) == 1   # negative count
+    hist[0, 3] = 11
+    assert lib.lsb_plan_exchange(10, P, 0, nb, hist.ctypes.data, *ptrs) == 1   # counts exceed n

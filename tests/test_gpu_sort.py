@@ -271,6 +271,30 @@ def test_exchange_slices(lsb_built, oracle_mod, slices, n, P, bits):
         assert np.array_equal(w.gather_global(), oracle_mod.stable_sort(a))
 
 
+def test_error_codes_on_a_context(lsb_built):
+    """Bad arguments on a live context return LSB_ERR_INVALID and leave it usable."""
+    import ctypes
+    lib = lsb_built._lib()
+    with lsb_built.World(1000, ranks=2) as w:
+        h = w._h
+        buf = np.zeros(600, dtype=DT)
+        assert lib.lsb_copy_in(h, 2, 0, 1, buf.ctypes.data) == 1          # no rank 2
+        assert lib.lsb_copy_in(h, 0, 400, 101, buf.ctypes.data) == 1      # past per = 500
+        assert lib.lsb_copy_out(h, 0, -1, 1, buf.ctypes.data) == 1
+        assert lib.lsb_copy_in(h, 0, 0, 1, None) == 1
+        assert lib.lsb_pass(h, 8) == 1 and lib.lsb_pass(h, -1) == 1       # 8-bit: digits 0..7
+        assert lib.lsb_set_option(h, 99, 1) == 1
+        assert lib.lsb_generate_ex(h, 7, 0.0) == 1
+        assert lib.lsb_generate_ex(h, lsb_built.DIST_ZIPF, 0.0) == 1
+        assert lib.lsb_get_kernel_stats(h, 6, None, None) == 1
+        first, num = ctypes.c_int(), ctypes.c_int()
+        assert lib.lsb_local_ranks(h, ctypes.byref(first), ctypes.byref(num)) == 0
+        assert (first.value, num.value) == (0, 2)
+        w.generate()
+        w.my_sort()
+        assert w.verify() == (True, -1)
+
+
 def test_exchange_slices_option_range(lsb_built):
     with lsb_built.World(10, ranks=2) as w:
         for bad in (0, 65):
