@@ -41,7 +41,10 @@ using lsb::Elem;
 
 namespace {
 
-enum class Mode { kLoopback, kRccl };
+// kLoopback: all ranks in this process (lsb_create); kRccl: this process is
+// one rank, RCCL collectives (lsb_create_rank); kOps: one rank, the caller's
+// host collectives (lsb_create_rank_ops).
+enum class Mode { kLoopback, kRccl, kOps };
 
 struct PendingEvent {
   int kid;
@@ -92,6 +95,7 @@ struct lsb_ctx {
   int first_rank = 0;
   std::vector<Rank> ranks;  // local ranks
   ncclComm_t comm = nullptr;
+  lsb_comm_ops_t ops = {};  // Mode::kOps
   bool timing = false;
   bool force_exchange = false;
   bool skip_constant = true;  // lsb_sort skips digits on which all keys agree
@@ -492,7 +496,72 @@ int exchange_loopback(lsb_ctx* c, int digit) {
   return LSB_OK;
 }
 
-// ---- exchange: RCCL (one rank per process) ------------------------------
+// ---- collectives of a one-rank-per-process context -------------------------
+// RCCL on the rank's stream (Mode::kRccl), or the caller's host callbacks
+// (Mode::kOps: sync the stream, stage through host memory, call, copy back).
+int ops_fail(const char* what) { return fail(LSB_ERR_RCCL, what, "comm callback failed"); }
+
+// count u64 per rank into recv[P * count]; in place when send == recv + rank * count.
+int coll_allgather_u64(lsb_ctx* c, Rank& r, const uint64_t* send, uint64_t* recv, size_t count) {
+  if (c->mode == Mode::kRccl) {
+    RCCL_TRY(ncclAllGather(send, recv, count, ncclUint64, c->comm, r.stream));
+    return LSB_OK;
+  }
+  std::vector<uint64_t> hs(count), hr(count * c->P);
+  HIP_TRY(hipMemcpyAsync(hs.data(), send, count * 8, hipMemcpyDeviceToHost, r.stream));
+  HIP_TRY(hipStreamSynchronize(r.stream));
+  if (c->ops.allgather(c->ops.user, hs.data(), hr.data(), count * 8) != 0) return ops_fail("allgather");
+  HIP_TRY(hipMemcpyAsync(recv, hr.data(), count * 8 * c->P, hipMemcpyHostToDevice, r.stream));
+  HIP_TRY(hipStreamSynchronize(r.stream));
+  return LSB_OK;
+}
+
+// MPI_Alltoallv semantics in uint64 units (counts and displacements).
+int coll_alltoallv_u64(lsb_ctx* c, Rank& r, const uint64_t* send, const size_t* sc,
+                       const size_t* sd, uint64_t* recv, const size_t* rc, const size_t* rd) {
+  const int P = c->P;
+  if (c->mode == Mode::kRccl) {
+    if (!c->p2p) {
+      RCCL_TRY(ncclAllToAllv(send, sc, sd, recv, rc, rd, ncclUint64, c->comm, r.stream));
+    } else {  // the same exchange as explicit grouped point-to-point calls
+      RCCL_TRY(ncclGroupStart());
+      for (int q = 0; q < P; ++q) {
+        if (sc[q] > 0) RCCL_TRY(ncclSend(send + sd[q], sc[q], ncclUint64, q, c->comm, r.stream));
+        if (rc[q] > 0) RCCL_TRY(ncclRecv(recv + rd[q], rc[q], ncclUint64, q, c->comm, r.stream));
+      }
+      RCCL_TRY(ncclGroupEnd());
+    }
+    return LSB_OK;
+  }
+  size_t send_end = 0, recv_end = 0;
+  for (int q = 0; q < P; ++q) {
+    if (sc[q]) send_end = std::max(send_end, sd[q] + sc[q]);
+    if (rc[q]) recv_end = std::max(recv_end, rd[q] + rc[q]);
+  }
+  std::vector<uint64_t> hs(std::max<size_t>(send_end, 1)), hr(std::max<size_t>(recv_end, 1));
+  std::vector<size_t> sb(P), sdb(P), rb(P), rdb(P);
+  for (int q = 0; q < P; ++q) {
+    if (sc[q])
+      HIP_TRY(hipMemcpyAsync(hs.data() + sd[q], send + sd[q], sc[q] * 8, hipMemcpyDeviceToHost,
+                             r.stream));
+    sb[q] = sc[q] * 8;
+    sdb[q] = sd[q] * 8;
+    rb[q] = rc[q] * 8;
+    rdb[q] = rd[q] * 8;
+  }
+  HIP_TRY(hipStreamSynchronize(r.stream));
+  if (c->ops.alltoallv(c->ops.user, hs.data(), sb.data(), sdb.data(), hr.data(), rb.data(),
+                       rdb.data()) != 0)
+    return ops_fail("alltoallv");
+  for (int q = 0; q < P; ++q)
+    if (rc[q])
+      HIP_TRY(hipMemcpyAsync(recv + rd[q], hr.data() + rd[q], rc[q] * 8, hipMemcpyHostToDevice,
+                             r.stream));
+  HIP_TRY(hipStreamSynchronize(r.stream));
+  return LSB_OK;
+}
+
+// ---- exchange: one rank per process (RCCL, or the caller's collectives) ----
 int exchange_rccl(lsb_ctx* c, int digit) {
   const int shift = digit * c->bits;
   const int P = c->P;
@@ -503,7 +572,7 @@ int exchange_rccl(lsb_ctx* c, int digit) {
   HIP_TRY(hipSetDevice(r.dev));
   {
     Timer t(c, &r, LSB_K_EXCHANGE);
-    RCCL_TRY(ncclAllGather(counts, r.gather, nb, ncclUint64, c->comm, r.stream));
+    LSB_TRY(coll_allgather_u64(c, r, counts, r.gather, nb));
   }
   LSB_TRY(plan_launch(c, r));
   HIP_TRY(hipStreamSynchronize(r.stream));
@@ -527,17 +596,9 @@ int exchange_rccl(lsb_ctx* c, int digit) {
         sd[q] = (size_t)(r.send_displs[q] + slo) * 2;
         rdp[q] = (size_t)(r.recv_displs[q] + rlo) * 2;
       }
-      if (!c->p2p) {
-        RCCL_TRY(ncclAllToAllv(r.A, sc.data(), sd.data(), r.R, rc.data(), rdp.data(), ncclUint64,
-                               c->comm, r.stream));
-      } else {  // the same exchange as explicit grouped point-to-point calls
-        RCCL_TRY(ncclGroupStart());
-        for (int q = 0; q < P; ++q) {
-          if (sc[q] > 0) RCCL_TRY(ncclSend(r.A + sd[q] / 2, sc[q], ncclUint64, q, c->comm, r.stream));
-          if (rc[q] > 0) RCCL_TRY(ncclRecv(r.R + rdp[q] / 2, rc[q], ncclUint64, q, c->comm, r.stream));
-        }
-        RCCL_TRY(ncclGroupEnd());
-      }
+      LSB_TRY(coll_alltoallv_u64(c, r, reinterpret_cast<const uint64_t*>(r.A), sc.data(),
+                                 sd.data(), reinterpret_cast<uint64_t*>(r.R), rc.data(),
+                                 rdp.data()));
     }
     LSB_TRY(place_slice(c, r, shift, j));
   }
@@ -563,7 +624,7 @@ int do_pass(lsb_ctx* c, int digit, uint64_t varying = ~0ull, bool want_span = fa
   }
   if (!exchanging(c)) return LSB_OK;
   ++c->last_exchanges;
-  if (c->mode == Mode::kRccl) return exchange_rccl(c, digit);
+  if (c->mode != Mode::kLoopback) return exchange_rccl(c, digit);
   return exchange_loopback(c, digit);
 }
 
@@ -608,7 +669,7 @@ int gather_boundaries(lsb_ctx* c, std::vector<uint64_t>& bnd) {
                            hipMemcpyDeviceToDevice, r.stream));
   }
   // Each rank contributes its own 4 words (in-place all-gather).
-  RCCL_TRY(ncclAllGather(d + (size_t)r.rank * 4, d, 4, ncclUint64, c->comm, r.stream));
+  LSB_TRY(coll_allgather_u64(c, r, d + (size_t)r.rank * 4, d, 4));
   HIP_TRY(hipMemcpyAsync(bnd.data(), d, sizeof(uint64_t) * 4 * P, hipMemcpyDeviceToHost, r.stream));
   HIP_TRY(hipStreamSynchronize(r.stream));
   return LSB_OK;
@@ -616,6 +677,8 @@ int gather_boundaries(lsb_ctx* c, std::vector<uint64_t>& bnd) {
 
 int allreduce_min_i64(lsb_ctx* c, int64_t* v) {
   if (c->mode == Mode::kLoopback) return LSB_OK;
+  if (c->mode == Mode::kOps)
+    return c->ops.allreduce_min_i64(c->ops.user, v) == 0 ? LSB_OK : ops_fail("allreduce_min_i64");
   Rank& r = c->ranks[0];
   HIP_TRY(hipSetDevice(r.dev));
   int64_t* d = reinterpret_cast<int64_t*>(r.check);
@@ -630,10 +693,10 @@ int allreduce_min_i64(lsb_ctx* c, int64_t* v) {
 // complements over every rank (RCCL: all-gather of the 2 words per rank).
 int gather_span(lsb_ctx* c, uint64_t* kor, uint64_t* knor) {
   *kor = *knor = 0;
-  if (c->mode == Mode::kRccl) {
+  if (c->mode != Mode::kLoopback) {
     Rank& r = c->ranks[0];
     HIP_TRY(hipSetDevice(r.dev));
-    RCCL_TRY(ncclAllGather(r.span, r.span_gather, 2, ncclUint64, c->comm, r.stream));
+    LSB_TRY(coll_allgather_u64(c, r, r.span, r.span_gather, 2));
     HIP_TRY(hipMemcpyAsync(r.span_h, r.span_gather, sizeof(uint64_t) * 2 * c->P,
                            hipMemcpyDeviceToHost, r.stream));
     HIP_TRY(hipStreamSynchronize(r.stream));
@@ -743,6 +806,30 @@ int lsb_create_rank(lsb_ctx_t** out, int64_t n_total, int num_ranks, int rank, i
       }
     }
   }
+  if (rc != LSB_OK) {
+    lsb_destroy(c);
+    return rc;
+  }
+  *out = c;
+  return LSB_OK;
+}
+
+int lsb_create_rank_ops(lsb_ctx_t** out, int64_t n_total, int num_ranks, int rank, int dev_id,
+                        int radix_bits, const lsb_comm_ops_t* ops) {
+  if (!out) return fail(LSB_ERR_INVALID, "lsb_create_rank_ops", "null out");
+  *out = nullptr;
+  if (n_total < 0 || num_ranks < 1 || num_ranks > 64 || rank < 0 || rank >= num_ranks || !ops ||
+      !ops->allgather || !ops->alltoallv || !ops->allreduce_min_i64 || !ops->barrier)
+    return fail(LSB_ERR_INVALID, "lsb_create_rank_ops", "n, P, rank or ops");
+  if (radix_bits != 8 && radix_bits != 16)
+    return fail(LSB_ERR_UNSUPPORTED, "lsb_create_rank_ops", "radix_bits must be 8 or 16");
+  lsb_ctx* c = new_ctx(n_total, num_ranks, radix_bits);
+  if (!c) return LSB_ERR_NOMEM;
+  c->mode = Mode::kOps;
+  c->ops = *ops;
+  c->first_rank = rank;
+  c->ranks.resize(1);
+  const int rc = init_rank(c, c->ranks[0], rank, dev_id);
   if (rc != LSB_OK) {
     lsb_destroy(c);
     return rc;
@@ -904,7 +991,9 @@ int lsb_sync(lsb_ctx_t* c) {
 
 int lsb_barrier(lsb_ctx_t* c) {
   LSB_TRY(lsb_sync(c));
-  if (c->mode != Mode::kRccl) return LSB_OK;
+  if (c->mode == Mode::kLoopback) return LSB_OK;
+  if (c->mode == Mode::kOps)
+    return c->ops.barrier(c->ops.user) == 0 ? LSB_OK : ops_fail("barrier");
   Rank& r = c->ranks[0];
   HIP_TRY(hipSetDevice(r.dev));
   RCCL_TRY(ncclAllReduce(r.check, r.check, 1, ncclUint64, ncclSum, c->comm, r.stream));

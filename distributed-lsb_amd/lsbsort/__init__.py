@@ -25,6 +25,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 from typing import Optional, Sequence
 
 import numpy as np
@@ -57,6 +58,64 @@ class LsbError(RuntimeError):
 _L = None
 
 
+# -- host collectives (lsb_comm_ops_t) -------------------------------------
+_ALLGATHER = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                              ctypes.c_size_t)
+_ALLTOALLV = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                              ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t),
+                              ctypes.c_void_p, ctypes.POINTER(ctypes.c_size_t),
+                              ctypes.POINTER(ctypes.c_size_t))
+_ALLREDUCE_MIN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64))
+_BARRIER = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p)
+
+
+class CommOps(ctypes.Structure):
+    _fields_ = [("user", ctypes.c_void_p), ("allgather", _ALLGATHER), ("alltoallv", _ALLTOALLV),
+                ("allreduce_min_i64", _ALLREDUCE_MIN), ("barrier", _BARRIER)]
+
+
+def _bytes_at(ptr, n):
+    if n == 0:
+        return np.zeros(0, dtype=np.uint8)
+    return np.ctypeslib.as_array((ctypes.c_uint8 * n).from_address(ptr))
+
+
+def _make_comm_ops(comm, P):
+    """lsb_comm_ops_t whose callbacks call the Python object `comm`."""
+    def guard(fn):
+        def wrapped(*a):
+            try:
+                fn(*a)
+                return 0
+            except Exception as e:  # a failed collective is an error code, not a crash
+                print(f"lsbsort comm callback failed: {e!r}", file=sys.stderr)
+                return 1
+        return wrapped
+
+    def allgather(_u, send, recv, nbytes):
+        _bytes_at(recv, nbytes * P)[:] = comm.allgather(_bytes_at(send, nbytes).copy())
+
+    def alltoallv(_u, send, sc, sd, recv, rc, rd):
+        scn = [sc[i] for i in range(P)]
+        sdn = [sd[i] for i in range(P)]
+        rcn = [rc[i] for i in range(P)]
+        rdn = [rd[i] for i in range(P)]
+        send_len = max([d + c for d, c in zip(sdn, scn) if c] or [0])
+        recv_len = max([d + c for d, c in zip(rdn, rcn) if c] or [0])
+        comm.alltoallv(_bytes_at(send, send_len), scn, sdn, _bytes_at(recv, recv_len), rcn, rdn)
+
+    def allreduce_min(_u, v):
+        v[0] = int(comm.allreduce_min(int(v[0])))
+
+    def barrier(_u):
+        comm.barrier()
+
+    keep = (_ALLGATHER(guard(allgather)), _ALLTOALLV(guard(alltoallv)),
+            _ALLREDUCE_MIN(guard(allreduce_min)), _BARRIER(guard(barrier)))
+    ops = CommOps(None, *keep)
+    return ops, keep
+
+
 def _lib() -> ctypes.CDLL:
     global _L
     if _L is None:
@@ -73,6 +132,8 @@ def _lib() -> ctypes.CDLL:
             "lsb_create": (i32, [ctypes.POINTER(vp), i64, i32, ctypes.POINTER(ctypes.c_int), i32]),
             "lsb_get_unique_id": (i32, [ctypes.c_char_p]),
             "lsb_create_rank": (i32, [ctypes.POINTER(vp), i64, i32, i32, i32, i32, ctypes.c_char_p]),
+            "lsb_create_rank_ops": (i32, [ctypes.POINTER(vp), i64, i32, i32, i32, i32,
+                                          ctypes.POINTER(CommOps)]),
             "lsb_destroy": (None, [vp]),
             "lsb_set_option": (i32, [vp, i32, i64]),
             "lsb_get_last_sort": (i32, [vp, vp, vp, vp]),
@@ -180,6 +241,26 @@ class World:
         _check(_lib().lsb_create_rank(ctypes.byref(h), n, num_ranks, rank, device, radix_bits,
                                       unique_id), "lsb_create_rank")
         return cls(n, _handle=h, _P=num_ranks, radix_bits=radix_bits)
+
+    @classmethod
+    def rank_ops(cls, n: int, num_ranks: int, rank: int, device: int, comm,
+                 radix_bits: int = 8) -> "World":
+        """One rank per process with host collectives instead of RCCL.
+
+        `comm` provides (numpy uint8 buffers, host memory):
+          allgather(send) -> P * len(send) bytes, rank-major
+          alltoallv(send, send_counts, send_displs, recv, recv_counts, recv_displs)  (bytes)
+          allreduce_min(int) -> int
+          barrier()
+        Any transport works (MPI, gloo, sockets); see lsb_create_rank_ops.
+        """
+        ops, keep = _make_comm_ops(comm, num_ranks)
+        h = ctypes.c_void_p()
+        _check(_lib().lsb_create_rank_ops(ctypes.byref(h), n, num_ranks, rank, device, radix_bits,
+                                          ctypes.byref(ops)), "lsb_create_rank_ops")
+        w = cls(n, _handle=h, _P=num_ranks, radix_bits=radix_bits)
+        w._comm_keep = (ops, keep)  # the callbacks must outlive the context
+        return w
 
     # -- lifecycle --------------------------------------------------------
     def close(self) -> None:

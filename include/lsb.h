@@ -31,6 +31,7 @@
 #ifndef LSB_H
 #define LSB_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -98,6 +99,26 @@ int  lsb_get_unique_id(unsigned char id[LSB_UNIQUE_ID_BYTES]);
 int  lsb_create_rank(lsb_ctx_t** ctx, int64_t n_total, int num_ranks, int rank,
                      int dev_id, int radix_bits,
                      const unsigned char id[LSB_UNIQUE_ID_BYTES]);
+/* One process per rank with caller-supplied collectives instead of RCCL (any
+ * transport: MPI, gloo, sockets).  The runtime runs exactly the per-rank code
+ * of lsb_create_rank; around each collective it synchronizes its stream and
+ * stages the data through host memory.  All pointers are host pointers, all
+ * sizes are bytes; every rank makes the same calls in the same order (as
+ * MPI requires); a callback returns 0 on success.  `user` is passed back. */
+typedef struct lsb_comm_ops {
+  void* user;
+  /* recv[r * bytes .. (r+1) * bytes) = send of rank r */
+  int (*allgather)(void* user, const void* send, void* recv, size_t bytes);
+  /* MPI_Alltoallv on bytes */
+  int (*alltoallv)(void* user, const void* send, const size_t* send_bytes,
+                   const size_t* send_displs, void* recv, const size_t* recv_bytes,
+                   const size_t* recv_displs);
+  /* *value = min over ranks */
+  int (*allreduce_min_i64)(void* user, int64_t* value);
+  int (*barrier)(void* user);
+} lsb_comm_ops_t;
+int  lsb_create_rank_ops(lsb_ctx_t** ctx, int64_t n_total, int num_ranks, int rank,
+                         int dev_id, int radix_bits, const lsb_comm_ops_t* ops);
 void lsb_destroy(lsb_ctx_t* ctx);
 int  lsb_set_option(lsb_ctx_t* ctx, int option, int64_t value);
 /* Ranks owned by this context: [*first_rank, *first_rank + *num_local). */
