@@ -57,6 +57,9 @@ def parse():
                     help="exchange digit width: 8 or 16 (default: 8 on 1 GPU, 16 on >1 GPU; "
                          "local passes are 8-bit either way)")
     ap.add_argument("--dist", choices=("uniform", "zipf"), default="uniform")
+    ap.add_argument("--transport", choices=("rccl", "gloo"), default="rccl",
+                    help="N > 1 collectives: RCCL over xGMI (the measurement), or gloo host "
+                         "callbacks (lsb_create_rank_ops) to rehearse the flow on fewer GPUs")
     ap.add_argument("--zipf-s", type=float, default=1.1)
     return ap.parse_args()
 
@@ -104,6 +107,59 @@ class Dist:
     def close(self):
         if self.dist:
             self.dist.destroy_process_group()
+
+
+class GlooComm:
+    """lsb_comm_ops_t over torch.distributed gloo, on host byte buffers.
+
+    For `--transport gloo` (rehearsing the N > 1 flow where RCCL is not
+    available, e.g. several ranks on one GPU) and the multi-process tests.
+    """
+
+    def __init__(self, dist, world, rank):
+        import torch
+        self.torch, self.dist, self.world, self.rank = torch, dist, world, rank
+
+    def allgather(self, send):
+        t = self.torch.from_numpy(send)
+        out = [self.torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(out, t)
+        return self.torch.cat(out).numpy()
+
+    def alltoallv(self, send, sc, sd, recv, rc, rd):
+        reqs, bufs = [], []
+        for q in range(self.world):
+            if q == self.rank:
+                if sc[q]:
+                    recv[rd[q]:rd[q] + rc[q]] = send[sd[q]:sd[q] + sc[q]]
+                continue
+            if sc[q]:
+                reqs.append(self.dist.isend(self.torch.from_numpy(send[sd[q]:sd[q] + sc[q]].copy()), q))
+            if rc[q]:
+                buf = self.torch.empty(rc[q], dtype=self.torch.uint8)
+                reqs.append(self.dist.irecv(buf, q))
+                bufs.append((buf, rd[q]))
+        for r in reqs:
+            r.wait()
+        for buf, off in bufs:
+            recv[off:off + buf.numel()] = buf.numpy()
+
+    def allreduce_min(self, v):
+        t = self.torch.tensor([v], dtype=self.torch.int64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN)
+        return int(t[0])
+
+    def barrier(self):
+        self.dist.barrier()
+
+
+def visible_devices():
+    """HIP devices this process can see (device_count does not initialize HIP)."""
+    try:
+        import torch
+        return torch.cuda.device_count()
+    except Exception:
+        return 1
 
 
 _TORCH_DEV = None
@@ -182,7 +238,13 @@ def main():
         N = d.world
     n_total = a.n_per_gpu * N
     radix = a.radix_bits or (8 if N == 1 else 16)
-    if d.world > 1:
+    device = d.local_rank
+    if d.world > 1 and a.transport == "gloo":
+        # Rehearsal: ranks may share GPUs; collectives go through gloo on the host.
+        device = d.local_rank % max(1, visible_devices())
+        w = lsbsort.World.rank_ops(n_total, N, d.rank, device, GlooComm(d.dist, d.world, d.rank),
+                                   radix_bits=radix)
+    elif d.world > 1:
         uid = lsbsort.get_unique_id() if d.rank == 0 else None
         uid = d.bcast_bytes(uid)
         w = lsbsort.World.rank(n_total, N, d.rank, d.local_rank, uid, radix_bits=radix)
@@ -190,7 +252,7 @@ def main():
         if N != 1:
             raise SystemExit("multi-GPU runs are launched one process per GPU (torch.distributed.run)")
         w = lsbsort.World(n_total, ranks=1, radix_bits=radix)
-    bind_device(d.local_rank)
+    bind_device(device)
 
     def step(timed):
         w.generate(a.dist, a.zipf_s)
@@ -223,13 +285,22 @@ def main():
     ms_per_step = total / a.steps * 1e3
     value = n_total * a.steps / total / 1e6
     launches, scatter_ms = stats["scatter"]
+    m = a.n_per_gpu
+    size = f"2^{m.bit_length() - 1}" if m > 0 and m & (m - 1) == 0 else str(m)
     if N == 1:
-        workload = f"configs[1]: sort of 2^30 16-byte records per GPU, 8-bit digits, 8 passes, {N} GPU(s)"
+        cfg = "configs[1]" if radix == 8 else "configs[4]"
+        workload = (f"{cfg}: sort of {size} 16-byte records per GPU, {radix}-bit digits, "
+                    f"{64 // radix} passes, {N} GPU(s)")
+        if radix == 16:
+            workload += " (each digit as two stable 8-bit sub-passes; no exchange)"
     else:
-        workload = (f"configs[2]: sort of {N} x 2^30 16-byte records block-partitioned over {N} GPUs, "
-                    f"8-bit local passes, {radix}-bit exchange digits ({64 // radix} RCCL all-to-alls)")
+        cfg = "configs[2]" if a.dist == "uniform" else "configs[3]"
+        workload = (f"{cfg}: sort of {N} x {size} 16-byte records block-partitioned over {N} GPUs, "
+                    f"8-bit local passes, {radix}-bit exchange digits ({64 // radix} all-to-alls)")
     if a.dist != "uniform":
         workload += f", zipf s={a.zipf_s} keys"
+    if m != 1 << 30:
+        workload = "custom size, " + workload
     roof = None
     if launches and scatter_ms > 0:
         elems_per_launch = scatter_elems / launches
@@ -259,7 +330,7 @@ def main():
         "config": {"workload": workload, "n_total": n_total, "n_per_gpu": a.n_per_gpu,
                    "local_digit_bits": 8, "local_passes": 8, "exchange_digit_bits": radix if N > 1 else None,
                    "record_bytes": 16, "dist": a.dist,
-                   "parallelism": f"block partition over {N} GPU(s); per exchange digit RCCL AllGather of counts + Send/Recv all-to-all" if N > 1 else "1 GPU, no exchange"},
+                   "parallelism": (f"block partition over {N} GPU(s); per exchange digit RCCL AllGather of counts + AllToAllv in 4 slices" if a.transport == "rccl" else f"{N} ranks, gloo host collectives (rehearsal, not a measurement)") if N > 1 else "1 GPU, no exchange"},
         "roofline": roof,
         "sort_hbm_frac": round(sort_gbs / HBM_PEAK_GBS, 4),
         "kernel_ms_per_step": {k: round(v[1] / a.steps, 3) for k, v in stats.items()},

@@ -30,56 +30,17 @@ def _free_port():
     return port
 
 
-class GlooComm:
-    """lsb_comm_ops_t over torch.distributed (gloo), on host byte buffers."""
-
-    def __init__(self, dist, torch, world, rank):
-        self.dist, self.torch, self.world, self.rank = dist, torch, world, rank
-
-    def allgather(self, send):
-        t = self.torch.from_numpy(send)
-        out = [self.torch.empty_like(t) for _ in range(self.world)]
-        self.dist.all_gather(out, t)
-        return self.torch.cat(out).numpy()
-
-    def alltoallv(self, send, sc, sd, recv, rc, rd):
-        reqs, bufs = [], []
-        for q in range(self.world):
-            if q == self.rank:
-                if sc[q]:
-                    recv[rd[q]:rd[q] + rc[q]] = send[sd[q]:sd[q] + sc[q]]
-                continue
-            if sc[q]:
-                reqs.append(self.dist.isend(self.torch.from_numpy(send[sd[q]:sd[q] + sc[q]].copy()), q))
-            if rc[q]:
-                buf = self.torch.empty(rc[q], dtype=self.torch.uint8)
-                reqs.append(self.dist.irecv(buf, q))
-                bufs.append((buf, rd[q]))
-        for r in reqs:
-            r.wait()
-        for buf, off in bufs:
-            recv[off:off + buf.numel()] = buf.numpy()
-
-    def allreduce_min(self, v):
-        t = self.torch.tensor([v], dtype=self.torch.int64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN)
-        return int(t[0])
-
-    def barrier(self):
-        self.dist.barrier()
-
-
 def _worker(rank, world, port, case, result_dir):
-    for p in (os.path.join(ROOT, "distributed-lsb_amd"), os.path.join(ROOT, "oracle")):
+    for p in (ROOT, os.path.join(ROOT, "distributed-lsb_amd"), os.path.join(ROOT, "oracle")):
         sys.path.insert(0, p)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    import torch
     import torch.distributed as dist
     import lsbsort
+    from bench import GlooComm  # lsb_comm_ops_t over gloo (bench.py --transport gloo)
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
     n, bits, slices, mask = case["n"], case["bits"], case["slices"], case["mask"]
-    w = lsbsort.World.rank_ops(n, world, rank, 0, GlooComm(dist, torch, world, rank), radix_bits=bits)
+    w = lsbsort.World.rank_ops(n, world, rank, 0, GlooComm(dist, world, rank), radix_bits=bits)
     w.set_option(lsbsort.OPT_EXCHANGE_SLICES, slices)
     if mask is None:
         w.generate()  # pcg64(rank), as mpi_lsbsort.cpp:650-656
