@@ -78,9 +78,10 @@ hipError_t launch_starts_to_counts(const int64_t* first16, int64_t m, uint64_t* 
 
 // Receiver-side placement of one source's received range: src[i] (receive
 // index k0 + i) goes to out[off_row[digit] + k0 + i], off_row = the source's
-// row of the placement table (place_off[s * nbuckets ...]).
-hipError_t launch_place(const Elem* src, Elem* out, int64_t k0, int64_t count, int shift,
-                        int nbuckets, const int64_t* off_row, hipStream_t s);
+// row of the placement table (place_off[s * nbuckets ...]); out holds
+// out_len records (the receive order [k0, k0 + count) lies inside it).
+hipError_t launch_place(const Elem* src, Elem* out, int64_t out_len, int64_t k0, int64_t count,
+                        int shift, int nbuckets, const int64_t* off_row, hipStream_t s);
 
 // Exchange plan of rank `me` on device from the all-gathered counts
 // hist[s * nb + b] (same rule as the host planner lsb_plan_exchange):

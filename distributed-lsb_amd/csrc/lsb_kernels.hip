@@ -19,6 +19,15 @@
 //     16-byte stores from consecutive lanes.
 #include "lsb_kernels.h"
 
+// Debug build (make debug, -DLSB_DEBUG): device-side bounds asserts on every
+// scattered store.  A failing assert prints and traps the kernel.
+#ifdef LSB_DEBUG
+#include <cassert>
+#define LSB_DASSERT(c) assert(c)
+#else
+#define LSB_DASSERT(c) ((void)0)
+#endif
+
 namespace lsb {
 namespace {
 
@@ -455,13 +464,19 @@ __global__ __launch_bounds__(BLOCK, 2) void k_scatter(const Elem* __restrict__ i
       const Elem x = stage[j];
       const uint32_t d = (uint32_t)(x.key >> shift) & (kBuckets - 1);
       const int64_t g = delta[d] + j;
-      if (g < lim[d]) store_elem(out + g, x);
+      if (g < lim[d]) {
+        LSB_DASSERT(g >= 0 && g < m);
+        store_elem(out + g, x);
+      }
     }
     // The carried head of each line goes out in the same phase as its rest.
     if (flush_carry) {
 #pragma unroll
       for (int i = 0; i < CY; ++i)
-        if ((uint32_t)i < cy_len) store_elem(out + A + i, cy[i]);
+        if ((uint32_t)i < cy_len) {
+          LSB_DASSERT(A + i >= 0 && A + i < m);
+          store_elem(out + A + i, cy[i]);
+        }
     }
     __syncthreads();
 
@@ -510,7 +525,8 @@ template <bool kLds>
 __global__ __launch_bounds__(kPlaceBlock) void k_place(const Elem* __restrict__ src,
                                                        Elem* __restrict__ out, int64_t k0,
                                                        int64_t count, int shift, uint32_t mask,
-                                                       const int64_t* __restrict__ off_row) {
+                                                       const int64_t* __restrict__ off_row,
+                                                       int64_t out_len) {
   __shared__ int64_t lds_off[kLds ? kPlaceLdsBuckets : 1];
   const int nb = (int)mask + 1;
   const int64_t* off = off_row;
@@ -535,6 +551,7 @@ __global__ __launch_bounds__(kPlaceBlock) void k_place(const Elem* __restrict__ 
       const int64_t k = base + (int64_t)i * kPlaceBlock;
       if (k < count) {
         const uint32_t d = (uint32_t)(x[i].key >> shift) & mask;
+        LSB_DASSERT(off[d] + k0 + k >= 0 && off[d] + k0 + k < out_len);
         store_elem(out + (off[d] + k0 + k), x[i]);
       }
     }
@@ -858,18 +875,19 @@ hipError_t launch_scatter(const Elem* in, Elem* out, int64_t m, int shift, Chunk
   return hipGetLastError();
 }
 
-hipError_t launch_place(const Elem* src, Elem* out, int64_t k0, int64_t count, int shift,
-                        int nbuckets, const int64_t* off_row, hipStream_t s) {
+hipError_t launch_place(const Elem* src, Elem* out, int64_t out_len, int64_t k0, int64_t count,
+                        int shift, int nbuckets, const int64_t* off_row, hipStream_t s) {
   if (count <= 0) return hipSuccess;
   if (nbuckets != 256 && nbuckets != 65536) return hipErrorInvalidValue;
+  if (k0 < 0 || k0 + count > out_len) return hipErrorInvalidValue;
   const dim3 grid(grid_for(count, kPlaceBlock * kPlaceIpt, 4096));
   const uint32_t mask = (uint32_t)nbuckets - 1;
   if (nbuckets <= kPlaceLdsBuckets)
     hipLaunchKernelGGL(k_place<true>, grid, dim3(kPlaceBlock), 0, s, src, out, k0, count, shift,
-                       mask, off_row);
+                       mask, off_row, out_len);
   else
     hipLaunchKernelGGL(k_place<false>, grid, dim3(kPlaceBlock), 0, s, src, out, k0, count, shift,
-                       mask, off_row);
+                       mask, off_row, out_len);
   return hipGetLastError();
 }
 

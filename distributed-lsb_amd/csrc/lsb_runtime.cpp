@@ -405,7 +405,7 @@ int place_range(lsb_ctx* c, Rank& r, int shift, int src_rank, const Elem* src, i
                 int64_t cnt) {
   if (cnt <= 0) return LSB_OK;
   Timer t(c, &r, LSB_K_PLACE, r.pstream);
-  HIP_TRY(lsb::launch_place(src, r.B, k0, cnt, shift, c->nb,
+  HIP_TRY(lsb::launch_place(src, r.B, r.here, k0, cnt, shift, c->nb,
                             r.place + (size_t)src_rank * c->nb, r.pstream));
   return LSB_OK;
 }
