@@ -16,8 +16,12 @@ static_assert(sizeof(Elem) == 16, "16-byte records");
 
 constexpr int kDigitBits = 8;                 // one local pass = one 8-bit digit
 constexpr int kBuckets = 1 << kDigitBits;     // 256
-constexpr int kScatterBlock = 256;            // 4 waves
-constexpr int kScatterIpt = 16;               // items per thread
+#ifndef LSB_SCATTER_BLOCK
+#define LSB_SCATTER_BLOCK 256
+#define LSB_SCATTER_IPT 16
+#endif
+constexpr int kScatterBlock = LSB_SCATTER_BLOCK;  // 4 waves
+constexpr int kScatterIpt = LSB_SCATTER_IPT;      // items per thread
 constexpr int kTile = kScatterBlock * kScatterIpt;  // 4096 elements = 64 KiB in LDS
 constexpr int kMaxChunks = 65536;             // upper bound on the chunk grid
 

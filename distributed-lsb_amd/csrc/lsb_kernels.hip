@@ -342,7 +342,7 @@ constexpr int kLineElems = 8;  // 128-B line / 16-B record
 // run's first record needs a look (by its bucket's thread, once per tile).
 // The rare tile across a low-byte boundary walks its runs.
 template <int BLOCK, int IPT, bool STARTS>
-__global__ __launch_bounds__(BLOCK, 2) void k_scatter(const Elem* __restrict__ in,
+__global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_scatter(const Elem* __restrict__ in,
                                                       Elem* __restrict__ out, int64_t m,
                                                       int shift, int64_t chunk_elems, int G,
                                                       const uint64_t* __restrict__ chunk_off,
