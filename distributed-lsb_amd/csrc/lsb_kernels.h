@@ -87,6 +87,15 @@ hipError_t launch_starts_to_counts(const int64_t* first16, int64_t m, uint64_t* 
 hipError_t launch_place(const Elem* src, Elem* out, int64_t out_len, int64_t k0, int64_t count,
                         int shift, int nbuckets, const int64_t* off_row, hipStream_t s);
 
+// Peer-store exchange (opt-in, LSB_OPT_EXCHANGE_PEER): from the all-gathered
+// counts hist[s * nb + b], rank `me` writes each of its m bucket-ordered
+// records straight into its owner's receiving buffer: record i of bucket b
+// goes to global position g = base[b] + i, i.e. dst[g / per][g % per].
+// dst[q] is rank q's buffer as this process sees it; base: nb int64 scratch.
+hipError_t launch_peer_exchange(const Elem* src, int64_t m, int shift, int nbuckets,
+                                const uint64_t* hist, int P, int me, int64_t per,
+                                Elem* const* dst, int64_t* base, hipStream_t s);
+
 // Exchange plan of rank `me` on device from the all-gathered counts
 // hist[s * nb + b] (same rule as the host planner lsb_plan_exchange):
 // place[s * nb + b] = place_off, place[P * nb + s] = rend (inclusive scan of

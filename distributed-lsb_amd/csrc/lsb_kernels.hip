@@ -558,6 +558,87 @@ __global__ __launch_bounds__(kPlaceBlock) void k_place(const Elem* __restrict__ 
   }
 }
 
+// ------------------------------------------ peer-store exchange (opt-in)
+// The SHMEM / MPI-RMA form of the exchange (shmem/shmem_lsbsort.cpp:441-456
+// shmem_putmem, mpi/mpi_lsbsort_onesided.cpp:487-509 MPI_Put): the sender
+// writes each record straight into its owner's next A.  Record i of my
+// bucket-ordered buffer, in bucket b, has global position g = base[b] + i,
+// base[b] = (global start of (b, me) in digit-major, rank-minor order) -
+// (local start of b); owner q = g / per, slot g - q * per.
+struct PeerDests {
+  Elem* dst[64];  // rank q's receiving buffer (this process's view of it)
+};
+
+constexpr int kPeerBaseBlock = 1024;
+
+// One workgroup: base[b] for b < nb from the all-gathered counts hist[s * nb + b].
+__global__ __launch_bounds__(kPeerBaseBlock) void k_peer_base(const uint64_t* __restrict__ hist,
+                                                              int P, int nb, int me,
+                                                              int64_t* __restrict__ base) {
+  __shared__ uint64_t tmp_t[kPeerBaseBlock / 64], tmp_m[kPeerBaseBlock / 64];
+  const int t = threadIdx.x;
+  const int per_t = (nb + kPeerBaseBlock - 1) / kPeerBaseBlock;
+  const int b0 = t * per_t, b1 = min(nb, b0 + per_t);
+  uint64_t tot = 0, mine = 0;
+  for (int b = b0; b < b1; ++b) {
+    for (int s = 0; s < P; ++s) tot += hist[(int64_t)s * nb + b];
+    mine += hist[(int64_t)me * nb + b];
+  }
+  uint64_t all_t, all_m;
+  uint64_t gt = block_exclusive_scan<kPeerBaseBlock>(tot, tmp_t, &all_t);
+  uint64_t gm = block_exclusive_scan<kPeerBaseBlock>(mine, tmp_m, &all_m);
+  for (int b = b0; b < b1; ++b) {
+    uint64_t before = 0, tb = 0;
+    for (int s = 0; s < P; ++s) {
+      const uint64_t h = hist[(int64_t)s * nb + b];
+      if (s < me) before += h;
+      tb += h;
+    }
+    base[b] = (int64_t)(gt + before) - (int64_t)gm;
+    gt += tb;
+    gm += hist[(int64_t)me * nb + b];
+  }
+}
+
+template <bool kLds>
+__global__ __launch_bounds__(kPlaceBlock) void k_peer_scatter(const Elem* __restrict__ src,
+                                                              int64_t m, int shift, uint32_t mask,
+                                                              const int64_t* __restrict__ base_g,
+                                                              int64_t per, int P, PeerDests d) {
+  __shared__ int64_t lds_base[kLds ? kPlaceLdsBuckets : 1];
+  const int nb = (int)mask + 1;
+  const int64_t* base = base_g;
+  if (kLds) {
+    for (int i = threadIdx.x; i < nb; i += kPlaceBlock) lds_base[i] = base_g[i];
+    __syncthreads();
+    base = lds_base;
+  }
+  const double inv_per = 1.0 / (double)per;
+  const int64_t step = (int64_t)gridDim.x * kPlaceBlock * kPlaceIpt;
+  for (int64_t i0 = (int64_t)blockIdx.x * kPlaceBlock * kPlaceIpt + threadIdx.x; i0 < m;
+       i0 += step) {
+    Elem x[kPlaceIpt];
+#pragma unroll
+    for (int j = 0; j < kPlaceIpt; ++j) {
+      const int64_t i = i0 + (int64_t)j * kPlaceBlock;
+      x[j] = i < m ? load_elem(src + i) : Elem{0ull, 0ull};
+    }
+#pragma unroll
+    for (int j = 0; j < kPlaceIpt; ++j) {
+      const int64_t i = i0 + (int64_t)j * kPlaceBlock;
+      if (i < m) {
+        const uint32_t b = (uint32_t)(x[j].key >> shift) & mask;
+        const int64_t g = base[b] + i;
+        int q = (int)((double)g * inv_per);  // then exact: q * per <= g < (q + 1) * per
+        if ((int64_t)q * per > g) --q;
+        if ((int64_t)(q + 1) * per <= g) ++q;
+        LSB_DASSERT(q >= 0 && q < P);
+        store_elem(d.dst[q] + (g - (int64_t)q * per), x[j]);
+      }
+    }
+  }
+}
+
 // --------------------------------------------- 16-bit digit counts (P > 1)
 // After the two 8-bit local sub-passes of a 16-bit digit the rank's records
 // are sorted by that digit, so its 65536-bin histogram is the run lengths:
@@ -888,6 +969,26 @@ hipError_t launch_place(const Elem* src, Elem* out, int64_t out_len, int64_t k0,
   else
     hipLaunchKernelGGL(k_place<false>, grid, dim3(kPlaceBlock), 0, s, src, out, k0, count, shift,
                        mask, off_row, out_len);
+  return hipGetLastError();
+}
+
+hipError_t launch_peer_exchange(const Elem* src, int64_t m, int shift, int nbuckets,
+                                const uint64_t* hist, int P, int me, int64_t per,
+                                Elem* const* dst, int64_t* base, hipStream_t s) {
+  if (P < 1 || P > 64 || me < 0 || me >= P || (nbuckets != 256 && nbuckets != 65536))
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_peer_base, dim3(1), dim3(kPeerBaseBlock), 0, s, hist, P, nbuckets, me, base);
+  if (m <= 0) return hipGetLastError();
+  PeerDests d{};
+  for (int q = 0; q < P; ++q) d.dst[q] = dst[q];
+  const dim3 grid(grid_for(m, kPlaceBlock * kPlaceIpt, 4096));
+  const uint32_t mask = (uint32_t)nbuckets - 1;
+  if (nbuckets <= kPlaceLdsBuckets)
+    hipLaunchKernelGGL(k_peer_scatter<true>, grid, dim3(kPlaceBlock), 0, s, src, m, shift, mask,
+                       base, per, P, d);
+  else
+    hipLaunchKernelGGL(k_peer_scatter<false>, grid, dim3(kPlaceBlock), 0, s, src, m, shift, mask,
+                       base, per, P, d);
   return hipGetLastError();
 }
 

@@ -80,6 +80,13 @@ struct Rank {
   uint64_t* span_h = nullptr;           // [2P] pinned host mirror
   int64_t* counts_h = nullptr;          // pinned host mirror of plan_counts
   lsb::Chunking chunking;
+  // Peer-store exchange (LSB_OPT_EXCHANGE_PEER): the two physical record
+  // buffers (A and B swap between them), every rank's two buffers as this
+  // process sees them (IPC-opened for other processes), and the base table.
+  Elem* buf[2] = {nullptr, nullptr};
+  std::vector<Elem*> peer0, peer1;
+  std::vector<void*> ipc_opened;
+  int64_t* peer_base = nullptr;         // [nb]
   std::vector<int64_t> send_counts, send_displs, recv_counts, recv_displs;
 };
 
@@ -101,6 +108,8 @@ struct lsb_ctx {
   bool skip_constant = true;  // lsb_sort skips digits on which all keys agree
   int slices = 4;             // exchange slices (placement overlaps the next slice)
   bool p2p = false;           // RCCL exchange as grouped ncclSend/ncclRecv, not ncclAllToAllv
+  bool peer = false;          // exchange by direct stores into the owners' buffers
+  bool peer_ready = false;    // peer tables set up
   // What the last lsb_sort ran (lsb_get_last_sort).
   int last_local_passes = 0;
   int last_exchanges = 0;
@@ -245,6 +254,8 @@ int init_rank(lsb_ctx* c, Rank& r, int rank, int dev) {
   const size_t P = (size_t)c->P, nb = (size_t)c->nb;
   LSB_TRY(dev_alloc(&r.A, per));
   LSB_TRY(dev_alloc(&r.B, per));
+  r.buf[0] = r.A;
+  r.buf[1] = r.B;
   if (c->P > 1) LSB_TRY(dev_alloc(&r.R, per));
   LSB_TRY(dev_alloc(&r.chunk_hist, hist_entries));
   LSB_TRY(dev_alloc(&r.chunk_off, hist_entries));
@@ -275,6 +286,8 @@ void free_rank(Rank& r) {
     (void)hipSetDevice(r.dev);
     (void)hipStreamSynchronize(r.stream);
   }
+  for (void* p : r.ipc_opened) (void)hipIpcCloseMemHandle(p);
+  (void)hipFree(r.peer_base);
   (void)hipFree(r.A);
   (void)hipFree(r.B);
   (void)hipFree(r.R);
@@ -561,6 +574,138 @@ int coll_alltoallv_u64(lsb_ctx* c, Rank& r, const uint64_t* send, const size_t* 
   return LSB_OK;
 }
 
+// ---- exchange: peer stores (opt-in, LSB_OPT_EXCHANGE_PEER) ----------------
+// Each rank writes its records straight into its owners' receiving buffers
+// (shmem_putmem / MPI_Put in the reference, shmem/shmem_lsbsort.cpp:441-456,
+// mpi/mpi_lsbsort_onesided.cpp:487-509): no R buffer, no all-to-all, no
+// placement pass.  Ordering: the counts all-gather cannot complete before
+// every rank's local pass has (stream order), so no store lands in a buffer
+// still being read; a barrier after the stores orders them before any
+// rank's next pass.  Visibility across GPUs relies on kernel boundaries
+// writing back / invalidating L2 (required on MI300-class parts even within
+// one device, whose XCDs have separate L2s).
+
+// Every rank's two physical buffers as this process sees them.
+int peer_setup(lsb_ctx* c) {
+  if (c->peer_ready) return LSB_OK;
+  const int P = c->P;
+  if (c->mode == Mode::kLoopback) {
+    for (Rank& r : c->ranks) {
+      r.peer0.assign(P, nullptr);
+      r.peer1.assign(P, nullptr);
+      HIP_TRY(hipSetDevice(r.dev));
+      for (Rank& q : c->ranks) {
+        r.peer0[q.rank] = q.buf[0];
+        r.peer1[q.rank] = q.buf[1];
+        if (q.dev != r.dev) {
+          hipError_t e = hipDeviceEnablePeerAccess(q.dev, 0);
+          if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+            return fail(LSB_ERR_HIP, "hipDeviceEnablePeerAccess", hipGetErrorString(e));
+          (void)hipGetLastError();
+        }
+      }
+    }
+    c->peer_ready = true;
+    return LSB_OK;
+  }
+  // One rank per process: IPC handles of both buffers, all-gathered.
+  Rank& r = c->ranks[0];
+  HIP_TRY(hipSetDevice(r.dev));
+  static_assert(sizeof(hipIpcMemHandle_t) % 8 == 0, "handle in u64 words");
+  constexpr size_t kW = sizeof(hipIpcMemHandle_t) / 8;  // words per handle
+  std::vector<uint64_t> mine(2 * kW), all((size_t)P * 2 * kW);
+  HIP_TRY(hipIpcGetMemHandle(reinterpret_cast<hipIpcMemHandle_t*>(mine.data()), r.buf[0]));
+  HIP_TRY(hipIpcGetMemHandle(reinterpret_cast<hipIpcMemHandle_t*>(mine.data() + kW), r.buf[1]));
+  uint64_t* d = r.gather;  // >= P * 2 * kW words (P * nb, nb >= 256)
+  HIP_TRY(hipMemcpyAsync(d + (size_t)r.rank * 2 * kW, mine.data(), 2 * kW * 8,
+                         hipMemcpyHostToDevice, r.stream));
+  LSB_TRY(coll_allgather_u64(c, r, d + (size_t)r.rank * 2 * kW, d, 2 * kW));
+  HIP_TRY(hipMemcpyAsync(all.data(), d, all.size() * 8, hipMemcpyDeviceToHost, r.stream));
+  HIP_TRY(hipStreamSynchronize(r.stream));
+  r.peer0.assign(P, nullptr);
+  r.peer1.assign(P, nullptr);
+  for (int q = 0; q < P; ++q) {
+    if (q == r.rank) {
+      r.peer0[q] = r.buf[0];
+      r.peer1[q] = r.buf[1];
+      continue;
+    }
+    for (int k = 0; k < 2; ++k) {
+      hipIpcMemHandle_t h;
+      memcpy(&h, all.data() + ((size_t)q * 2 + k) * kW, sizeof h);
+      void* p = nullptr;
+      HIP_TRY(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+      r.ipc_opened.push_back(p);
+      (k == 0 ? r.peer0 : r.peer1)[q] = static_cast<Elem*>(p);
+    }
+  }
+  c->peer_ready = true;
+  return LSB_OK;
+}
+
+// All ranks' stores are done: loopback waits for every stream, one rank per
+// process runs a barrier collective after its own stores.
+int peer_barrier(lsb_ctx* c) {
+  if (c->mode == Mode::kLoopback) {
+    for (Rank& r : c->ranks) {
+      HIP_TRY(hipSetDevice(r.dev));
+      HIP_TRY(hipStreamSynchronize(r.stream));
+    }
+    return LSB_OK;
+  }
+  Rank& r = c->ranks[0];
+  HIP_TRY(hipSetDevice(r.dev));
+  if (c->mode == Mode::kRccl) {
+    RCCL_TRY(ncclAllReduce(r.check, r.check, 1, ncclUint64, ncclSum, c->comm, r.stream));
+    return LSB_OK;
+  }
+  HIP_TRY(hipStreamSynchronize(r.stream));
+  return c->ops.barrier(c->ops.user) == 0 ? LSB_OK : ops_fail("barrier");
+}
+
+int exchange_peer(lsb_ctx* c, int digit) {
+  const int shift = digit * c->bits;
+  const size_t nb = (size_t)c->nb;
+  LSB_TRY(peer_setup(c));
+  // counts of every rank into every local rank's gather matrix
+  if (c->mode == Mode::kLoopback) {
+    std::vector<const uint64_t*> counts(c->ranks.size(), nullptr);
+    for (Rank& r : c->ranks) LSB_TRY(digit_counts(c, r, digit, &counts[r.rank]));
+    for (Rank& r : c->ranks) {
+      HIP_TRY(hipSetDevice(r.dev));
+      HIP_TRY(hipStreamSynchronize(r.stream));
+    }
+    for (Rank& q : c->ranks) {
+      HIP_TRY(hipSetDevice(q.dev));
+      for (Rank& s : c->ranks)
+        HIP_TRY(hipMemcpyAsync(q.gather + (size_t)s.rank * nb, counts[s.rank],
+                               sizeof(uint64_t) * nb, hipMemcpyDefault, q.stream));
+    }
+  } else {
+    Rank& r = c->ranks[0];
+    const uint64_t* counts = nullptr;
+    LSB_TRY(digit_counts(c, r, digit, &counts));
+    HIP_TRY(hipSetDevice(r.dev));
+    Timer t(c, &r, LSB_K_EXCHANGE);
+    LSB_TRY(coll_allgather_u64(c, r, counts, r.gather, nb));
+  }
+  for (Rank& r : c->ranks) {
+    HIP_TRY(hipSetDevice(r.dev));
+    if (!r.peer_base) {
+      HIP_TRY(hipMalloc(reinterpret_cast<void**>(&r.peer_base), sizeof(int64_t) * nb));
+    }
+    // Every rank swaps alike, so B is the same physical buffer index everywhere.
+    const bool free1 = r.B == r.buf[1];
+    Timer t(c, &r, LSB_K_EXCHANGE);
+    HIP_TRY(lsb::launch_peer_exchange(r.A, r.here, shift, c->nb, r.gather, c->P, r.rank, c->per,
+                                      (free1 ? r.peer1 : r.peer0).data(), r.peer_base,
+                                      r.stream));
+  }
+  LSB_TRY(peer_barrier(c));
+  for (Rank& r : c->ranks) std::swap(r.A, r.B);
+  return LSB_OK;
+}
+
 // ---- exchange: one rank per process (RCCL, or the caller's collectives) ----
 int exchange_rccl(lsb_ctx* c, int digit) {
   const int shift = digit * c->bits;
@@ -624,6 +769,7 @@ int do_pass(lsb_ctx* c, int digit, uint64_t varying = ~0ull, bool want_span = fa
   }
   if (!exchanging(c)) return LSB_OK;
   ++c->last_exchanges;
+  if (c->peer) return exchange_peer(c, digit);
   if (c->mode != Mode::kLoopback) return exchange_rccl(c, digit);
   return exchange_loopback(c, digit);
 }
@@ -865,6 +1011,9 @@ int lsb_set_option(lsb_ctx_t* c, int option, int64_t value) {
       return LSB_OK;
     case LSB_OPT_SKIP_CONSTANT_DIGITS:
       c->skip_constant = value != 0;
+      return LSB_OK;
+    case LSB_OPT_EXCHANGE_PEER:
+      c->peer = value != 0;
       return LSB_OK;
     case LSB_OPT_EXCHANGE_P2P:
       c->p2p = value != 0;

@@ -46,6 +46,7 @@ DIST_UNIFORM, DIST_ZIPF = 0, 1
 K_UPSWEEP, K_SCAN, K_SCATTER, K_EXCHANGE, K_PLACE, K_SORT = range(6)
 KERNEL_NAMES = ("upsweep", "scan", "scatter", "exchange", "place", "sort")
 OPT_TIMING, OPT_FORCE_EXCHANGE, OPT_SKIP_CONSTANT_DIGITS, OPT_EXCHANGE_SLICES, OPT_EXCHANGE_P2P = 0, 1, 2, 3, 4
+OPT_EXCHANGE_PEER = 5
 
 
 class LsbError(RuntimeError):

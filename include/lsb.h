@@ -77,6 +77,10 @@ typedef struct lsb_ctx lsb_ctx_t;
                                       is in flight */
 #define LSB_OPT_EXCHANGE_P2P    4  /* RCCL contexts: 0 (default) ncclAllToAllv per slice,
                                       1 the same as grouped ncclSend/ncclRecv */
+#define LSB_OPT_EXCHANGE_PEER   5  /* 1: exchange by direct stores into the owners' buffers
+                                      (shmem_putmem / MPI_Put form; IPC-mapped across
+                                      processes); no receive buffer, no placement pass.
+                                      Opt-in: set on every rank before the first sort. */
 
 /* ---- geometry: DistributedArray::create (mpi/mpi_lsbsort.cpp:144-149) ---- */
 int64_t lsb_per_rank(int64_t n_total, int num_ranks);            /* ceil(n/P) */

@@ -42,6 +42,7 @@ def _worker(rank, world, port, case, result_dir):
     n, bits, slices, mask = case["n"], case["bits"], case["slices"], case["mask"]
     w = lsbsort.World.rank_ops(n, world, rank, 0, GlooComm(dist, world, rank), radix_bits=bits)
     w.set_option(lsbsort.OPT_EXCHANGE_SLICES, slices)
+    w.set_option(lsbsort.OPT_EXCHANGE_PEER, int(case.get("peer", 0)))
     if mask is None:
         w.generate()  # pcg64(rank), as mpi_lsbsort.cpp:650-656
     else:
@@ -80,6 +81,16 @@ def test_processes_reproduce_reference_digest(tmp_path, digests, oracle_mod, wor
     for m in meta:
         assert m[0] == 1 and m[1] == -1 and m[2] == 1  # verify ok on every rank, checkSorted
         assert m[4] == 64 // bits                       # one exchange per digit
+
+
+@pytest.mark.parametrize("world,bits", [(2, 8), (4, 16)])
+def test_processes_peer_store_exchange(tmp_path, digests, oracle_mod, world, bits):
+    """Peer stores through IPC-mapped buffers of the other processes."""
+    row = next(r for r in digests["rows"] if r["P"] == world)
+    out, meta = _run(tmp_path, world, dict(n=row["n"], bits=bits, slices=4, mask=None, peer=1))
+    assert oracle_mod.digest(out) == row["output"]
+    for m in meta:
+        assert m[0] == 1 and m[1] == -1 and m[2] == 1
 
 
 @pytest.mark.parametrize("world,bits,mask,passes,exchanges", [

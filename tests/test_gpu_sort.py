@@ -271,6 +271,56 @@ def test_exchange_slices(lsb_built, oracle_mod, slices, n, P, bits):
         assert np.array_equal(w.gather_global(), oracle_mod.stable_sort(a))
 
 
+# ------------------------------------------------ peer-store exchange (opt-in)
+@pytest.mark.parametrize("row", range(5))
+@pytest.mark.parametrize("bits", [8, 16])
+def test_peer_exchange_golden_digests(lsb_built, oracle_mod, digests, row, bits):
+    d = digests["rows"][row]
+    with lsb_built.World(d["n"], ranks=d["P"], radix_bits=bits) as w:
+        w.set_option(lsb_built.OPT_EXCHANGE_PEER, 1)
+        w.set_option(lsb_built.OPT_FORCE_EXCHANGE, 1)
+        w.generate()
+        w.my_sort()
+        assert oracle_mod.digest(w.gather_global()) == d["output"]
+        assert w.verify() == (True, -1)
+
+
+@pytest.mark.parametrize("name", ["all_equal", "two_keys", "hot_bucket", "zipf", "small_range"])
+@pytest.mark.parametrize("P,bits", [(3, 8), (8, 16)])
+def test_peer_exchange_distributions(lsb_built, oracle_mod, name, P, bits):
+    rng = np.random.default_rng(hash((name, P, bits)) & 0xFFFF)
+    a = _dist(name, 100_003, rng)
+    with lsb_built.World(a.size, ranks=P, radix_bits=bits) as w:
+        w.set_option(lsb_built.OPT_EXCHANGE_PEER, 1)
+        w.scatter_global(a)
+        w.my_sort()
+        assert np.array_equal(w.gather_global(), oracle_mod.stable_sort(a))
+
+
+@pytest.mark.parametrize("n,P", [(0, 3), (1, 4), (9, 8), (4096 * 3 + 1, 2)])
+def test_peer_exchange_tiny(lsb_built, oracle_mod, n, P):
+    a = _masked_keys(n, 0xF0F0F0F0F0F0F0F0, np.random.default_rng(n + P))
+    with lsb_built.World(n, ranks=P) as w:
+        w.set_option(lsb_built.OPT_EXCHANGE_PEER, 1)
+        w.scatter_global(a)
+        w.my_sort()
+        assert np.array_equal(w.gather_global(), oracle_mod.stable_sort(a))
+
+
+def test_peer_exchange_rccl_world_of_one(lsb_built, oracle_mod, digests):
+    d = next(r for r in digests["rows"] if r["P"] == 1)
+    w = lsb_built.World.rank(d["n"], 1, 0, 0, lsb_built.get_unique_id(), radix_bits=16)
+    try:
+        w.set_option(lsb_built.OPT_FORCE_EXCHANGE, 1)
+        w.set_option(lsb_built.OPT_EXCHANGE_PEER, 1)
+        w.generate()
+        w.my_sort()
+        w.sync()
+        assert oracle_mod.digest(w.copy_out(0)) == d["output"]
+    finally:
+        w.close()
+
+
 def test_error_codes_on_a_context(lsb_built):
     """Bad arguments on a live context return LSB_ERR_INVALID and leave it usable."""
     import ctypes
