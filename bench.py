@@ -60,6 +60,9 @@ def parse():
     ap.add_argument("--transport", choices=("rccl", "gloo"), default="rccl",
                     help="N > 1 collectives: RCCL over xGMI (the measurement), or gloo host "
                          "callbacks (lsb_create_rank_ops) to rehearse the flow on fewer GPUs")
+    ap.add_argument("--exchange", choices=("alltoallv", "p2p", "peer"), default="alltoallv",
+                    help="N > 1 element exchange: RCCL AllToAllv in slices (default), grouped "
+                         "ncclSend/ncclRecv, or direct peer stores into the owners' buffers")
     ap.add_argument("--zipf-s", type=float, default=1.1)
     return ap.parse_args()
 
@@ -253,6 +256,10 @@ def main():
             raise SystemExit("multi-GPU runs are launched one process per GPU (torch.distributed.run)")
         w = lsbsort.World(n_total, ranks=1, radix_bits=radix)
     bind_device(device)
+    if a.exchange == "p2p":
+        w.set_option(lsbsort.OPT_EXCHANGE_P2P, 1)
+    elif a.exchange == "peer":
+        w.set_option(lsbsort.OPT_EXCHANGE_PEER, 1)
 
     def step(timed):
         w.generate(a.dist, a.zipf_s)
@@ -330,7 +337,7 @@ def main():
         "config": {"workload": workload, "n_total": n_total, "n_per_gpu": a.n_per_gpu,
                    "local_digit_bits": 8, "local_passes": 8, "exchange_digit_bits": radix if N > 1 else None,
                    "record_bytes": 16, "dist": a.dist,
-                   "parallelism": (f"block partition over {N} GPU(s); per exchange digit RCCL AllGather of counts + AllToAllv in 4 slices" if a.transport == "rccl" else f"{N} ranks, gloo host collectives (rehearsal, not a measurement)") if N > 1 else "1 GPU, no exchange"},
+                   "parallelism": (f"block partition over {N} GPU(s); per exchange digit RCCL AllGather of counts + " + {"alltoallv": "AllToAllv in 4 slices", "p2p": "grouped Send/Recv in 4 slices", "peer": "direct peer stores (IPC)"}[a.exchange] if a.transport == "rccl" else f"{N} ranks, gloo host collectives (rehearsal, not a measurement)") if N > 1 else "1 GPU, no exchange"},
         "roofline": roof,
         "sort_hbm_frac": round(sort_gbs / HBM_PEAK_GBS, 4),
         "kernel_ms_per_step": {k: round(v[1] / a.steps, 3) for k, v in stats.items()},
