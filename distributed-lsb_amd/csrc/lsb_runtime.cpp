@@ -256,7 +256,8 @@ int init_rank(lsb_ctx* c, Rank& r, int rank, int dev) {
   LSB_TRY(dev_alloc(&r.B, per));
   r.buf[0] = r.A;
   r.buf[1] = r.B;
-  if (c->P > 1) LSB_TRY(dev_alloc(&r.R, per));
+  // R (the all-to-all receive buffer) is allocated on first use: a context
+  // that never runs the all-to-all (P = 1, peer stores) keeps its HBM.
   LSB_TRY(dev_alloc(&r.chunk_hist, hist_entries));
   LSB_TRY(dev_alloc(&r.chunk_off, hist_entries));
   LSB_TRY(dev_alloc(&r.totals, lsb::kBuckets));
@@ -430,6 +431,7 @@ int place_self(lsb_ctx* c, Rank& r, int shift) {
   if (r.send_counts[me] != r.recv_counts[me])
     return fail(LSB_ERR_STATE, "exchange", "self count mismatch");
   HIP_TRY(hipSetDevice(r.dev));
+  if (!r.R) LSB_TRY(dev_alloc(&r.R, (size_t)c->per));  // first all-to-all of this context
   HIP_TRY(hipEventRecord(r.pevent, r.stream));  // plan kernels done
   HIP_TRY(hipStreamWaitEvent(r.pstream, r.pevent, 0));
   return place_range(c, r, shift, me, r.A + r.send_displs[me], r.recv_displs[me],
@@ -1000,13 +1002,6 @@ int lsb_set_option(lsb_ctx_t* c, int option, int64_t value) {
       c->timing = value != 0;
       return LSB_OK;
     case LSB_OPT_FORCE_EXCHANGE:
-      if (value) {
-        for (Rank& r : c->ranks)
-          if (!r.R) {
-            HIP_TRY(hipSetDevice(r.dev));
-            LSB_TRY(dev_alloc(&r.R, (size_t)c->per));
-          }
-      }
       c->force_exchange = value != 0;
       return LSB_OK;
     case LSB_OPT_SKIP_CONSTANT_DIGITS:
