@@ -16,6 +16,9 @@
 //   --json     also print one machine-readable line.
 //   --radix-bits 8|16   exchange digit width (local passes are always 8-bit)
 //   --dist uniform|zipf [--zipf-s S]   key distribution of the same pcg64 stream
+//   --exchange alltoallv|p2p|peer  element exchange (default RCCL AllToAllv in
+//              slices; grouped Send/Recv; direct peer stores, the shmem_putmem form)
+//   --slices S  all-to-all slices whose placement overlaps the next slice
 #include <sys/wait.h>
 #include <unistd.h>
 
@@ -43,6 +46,8 @@ struct Options {
   int radix_bits = 8;
   int dist = LSB_DIST_UNIFORM;
   double zipf_s = 1.1;
+  int exchange_option = -1;  // --exchange: LSB_OPT_EXCHANGE_P2P / _PEER, or -1 (AllToAllv)
+  int slices = 0;            // --slices S (0: library default)
 };
 
 void flush_output() {
@@ -101,6 +106,8 @@ void print_array(World& w, const char* name, int64_t n_per_rank) {
 }
 
 int run(World& w, const Options& o) {
+  if (o.exchange_option >= 0) CHECK(lsb_set_option(w.ctx, o.exchange_option, 1));
+  if (o.slices > 0) CHECK(lsb_set_option(w.ctx, LSB_OPT_EXCHANGE_SLICES, o.slices));
   if (w.root()) {
     printf("Total number of HIP ranks: %d\n", w.P);
     printf("Problem size: %" PRId64 "\n", o.n);
@@ -222,6 +229,14 @@ int main(int argc, char* argv[]) {
     else if (a == "--json") o.json = true;
     else if (a == "--radix-bits") o.radix_bits = std::stoi(next());
     else if (a == "--zipf-s") o.zipf_s = std::stod(next());
+    else if (a == "--slices") o.slices = std::stoi(next());
+    else if (a == "--exchange") {
+      const std::string x = next();
+      if (x == "alltoallv") o.exchange_option = -1;
+      else if (x == "p2p") o.exchange_option = LSB_OPT_EXCHANGE_P2P;
+      else if (x == "peer") o.exchange_option = LSB_OPT_EXCHANGE_PEER;
+      else { fprintf(stderr, "unknown --exchange %s\n", x.c_str()); return 2; }
+    }
     else if (a == "--dist") {
       const std::string d = next();
       if (d == "zipf") o.dist = LSB_DIST_ZIPF;

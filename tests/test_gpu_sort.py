@@ -439,10 +439,11 @@ def test_beyond_32bit_indices(lsb_built):
 
 
 # ------------------------------------------------------------- the harness
-def test_harness_matches_reference_lines(lsb_built, ref_vectors):
+@pytest.mark.parametrize("extra", [[], ["--exchange", "peer"], ["--slices", "3", "--radix-bits", "16"]])
+def test_harness_matches_reference_lines(lsb_built, ref_vectors, extra):
     case = next(c for c in ref_vectors["cases"] if c["n"] == 1000003 and c["P"] == 4)
     exe = lsb_built.HARNESS_PATH
-    out = subprocess.run([exe, "--n", "1000003", "--ranks", "4", "--print"], check=True,
+    out = subprocess.run([exe, "--n", "1000003", "--ranks", "4", "--print"] + extra, check=True,
                          capture_output=True, text=True, timeout=300).stdout
     lines = out.splitlines()
     assert lines[0] == "Total number of HIP ranks: 4"
