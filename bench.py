@@ -39,7 +39,7 @@ import lsbsort  # noqa: E402
 METRIC = "Melem/s (16-byte elems) at 1/2/4/8 GPUs; per-pass HBM GB/s vs roofline"
 HBM_PEAK_GBS = 8000.0           # MI355X HBM3E spec (MI355X_MICROARCH.md)
 SCATTER_BYTES_PER_ELEM = 32     # 16 B read + 16 B written per record per pass
-PASS_BYTES_PER_ELEM = 48        # + 16 B histogram read
+COUNT_BYTES_PER_ELEM = 16       # histogram read of the keys' lines
 REF_MPI_MELEMS = 830.0          # mpi_lsbsort, 64 nodes x 128 cores, n = 2^36
 
 
@@ -64,6 +64,8 @@ def parse():
                     help="N > 1 element exchange: RCCL AllToAllv in slices (default), grouped "
                          "ncclSend/ncclRecv, or direct peer stores into the owners' buffers")
     ap.add_argument("--zipf-s", type=float, default=1.1)
+    ap.add_argument("--passes", choices=("onesweep", "reduce-scan"), default="onesweep",
+                    help="N = 1 pass form: single-read (look-back) or count + scan + scatter")
     return ap.parse_args()
 
 
@@ -187,13 +189,13 @@ def device_sync():
     torch.cuda.synchronize(_TORCH_DEV)
 
 
-def load_traffic(workload):
-    """Per-launch HBM bytes of k_scatter from the committed rocprofv3 PMC summary."""
+def load_traffic(workload, kernel):
+    """Per-launch HBM bytes of the dominant kernel from the committed rocprofv3 PMC summary."""
     path = os.path.join(ROOT, "profiles", "pmc_scatter.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        if d.get("workload") == workload:
+        if d.get("workload") == workload and d.get("kernel", "k_scatter") == kernel:
             return d.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
@@ -260,6 +262,8 @@ def main():
         w.set_option(lsbsort.OPT_EXCHANGE_P2P, 1)
     elif a.exchange == "peer":
         w.set_option(lsbsort.OPT_EXCHANGE_PEER, 1)
+    w.set_option(lsbsort.OPT_ONESWEEP, 1 if a.passes == "onesweep" else 0)
+    kernel = "k_onesweep" if (N == 1 and a.passes == "onesweep") else "k_scatter"
 
     def step(timed):
         w.generate(a.dist, a.zipf_s)
@@ -313,12 +317,16 @@ def main():
         elems_per_launch = scatter_elems / launches
         avg_s = scatter_ms / launches / 1e3
         achieved = SCATTER_BYTES_PER_ELEM * elems_per_launch / avg_s / 1e9
-        traffic = load_traffic(workload)
+        traffic = load_traffic(workload, kernel)
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": "k_scatter", "bytes_per_launch": int(SCATTER_BYTES_PER_ELEM * elems_per_launch),
+                "kernel": kernel, "bytes_per_launch": int(SCATTER_BYTES_PER_ELEM * elems_per_launch),
                 "avg_launch_ms": round(scatter_ms / launches, 4)}
-    sort_gbs = PASS_BYTES_PER_ELEM * 8 * (n_total / N) / (ms_per_step / 1e3) / 1e9
+    # Algorithmic bytes of a sort: 32 B per record per scatter launch, 16 B
+    # per count read (one per pass for reduce-then-scan, one per sort for
+    # single-read passes).
+    per_elem = (SCATTER_BYTES_PER_ELEM * launches + COUNT_BYTES_PER_ELEM * stats["upsweep"][0]) / a.steps
+    sort_gbs = per_elem * (n_total / N) / (ms_per_step / 1e3) / 1e9
     out = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -335,7 +343,9 @@ def main():
                  if a.dist == "uniform" else
                  f"synthetic: zipf(s={a.zipf_s}) keys drawn from the pcg64(rank) stream (build-defined, SURVEY 8d C4)"),
         "config": {"workload": workload, "n_total": n_total, "n_per_gpu": a.n_per_gpu,
-                   "local_digit_bits": 8, "local_passes": 8, "exchange_digit_bits": radix if N > 1 else None,
+                   "local_digit_bits": 8, "local_passes": 8,
+                   "pass_form": ("single-read (k_subhist once, k_onesweep per pass)" if kernel == "k_onesweep"
+                                 else "reduce-then-scan (k_upsweep, k_scan, k_scatter per pass)"), "exchange_digit_bits": radix if N > 1 else None,
                    "record_bytes": 16, "dist": a.dist,
                    "parallelism": (f"block partition over {N} GPU(s); per exchange digit RCCL AllGather of counts + " + {"alltoallv": "AllToAllv in 4 slices", "p2p": "grouped Send/Recv in 4 slices", "peer": "direct peer stores (IPC)"}[a.exchange] if a.transport == "rccl" else f"{N} ranks, gloo host collectives (rehearsal, not a measurement)") if N > 1 else "1 GPU, no exchange"},
         "roofline": roof,

@@ -80,6 +80,26 @@ hipError_t launch_starts_reset(int64_t* first16, hipStream_t s);
 hipError_t launch_starts_to_counts(const int64_t* first16, int64_t m, uint64_t* counts,
                                    hipStream_t s);
 
+// Single-read passes (P == 1; k_onesweep in lsb_kernels.hip).  The m records
+// are kTile-record tiles in kOnesweepSubs contiguous sub-arrays, sub-array x
+// = tiles [x*TT/8, (x+1)*TT/8).  sub_hist[x * 256 + b] = count of digit b
+// in sub-array x.
+constexpr int kOnesweepSubs = 8;
+constexpr int64_t kOnesweepMaxElems = int64_t(1) << 34;  // 32-bit look-back values
+inline int64_t onesweep_tiles(int64_t m) { return (m + kTile - 1) / kTile; }
+// sub_hist (zeroed here) of the digit at `shift`; span as for launch_upsweep.
+hipError_t launch_subhist(const Elem* A, int64_t m, int shift, int grid, uint32_t* sub_hist,
+                          uint64_t* span, hipStream_t s);
+// One stable pass in -> out on the digit at `shift`, offsets from sub_hist
+// plus a look-back over status (onesweep_tiles(m) * 256 words, zeroed once at
+// allocation; epoch >= 1, new for every launch).  next_shift >= 0: also
+// next_hist (zeroed here) = sub_hist of the digit at next_shift over out.
+// tile_ctr: kOnesweepSubs words of scratch; *err |= 1 if a look-back gave up.
+hipError_t launch_onesweep(const Elem* in, Elem* out, int64_t m, int shift, int next_shift,
+                           const uint32_t* sub_hist, uint32_t* next_hist, uint64_t* status,
+                           uint32_t* tile_ctr, uint32_t epoch, uint32_t* err, int grid,
+                           hipStream_t s);
+
 // Receiver-side placement of one source's received range: src[i] (receive
 // index k0 + i) goes to out[off_row[digit] + k0 + i], off_row = the source's
 // row of the placement table (place_off[s * nbuckets ...]); out holds

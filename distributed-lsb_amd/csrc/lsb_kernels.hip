@@ -512,6 +512,334 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_scatter(const Elem* __re
   }
 }
 
+// ---------------------------------------------------------------- onesweep
+// Single-read passes for P == 1 (the same stable counting pass,
+// mpi/mpi_lsbsort.cpp:213-247, without the count re-read).  Reduce-then-scan
+// reads every record twice per pass (k_upsweep, k_scatter) only to learn
+// each chunk's bucket offsets.  Here those come from a decoupled look-back
+// and from a histogram the previous pass produced as it wrote:
+//
+//   * The m records are kTile-record tiles, grouped into kSub = 8 contiguous
+//     sub-arrays: sub-array x = tiles [x*TT/8, (x+1)*TT/8) (floor), so tile
+//     t lies in sub-array (8t + 7) / TT.  Workgroups with the same
+//     blockIdx % 8 share an XCD; that group takes sub-array blockIdx % 8's
+//     tiles in order from its own counter, then helps the next sub-array
+//     (the tail balances itself).  Consecutive tiles of a run boundary thus
+//     mostly complete their shared 128-B lines in one XCD's L2.
+//   * Record (tile t, bucket b) goes to bucket_start[b] + sub_pre[x][b] +
+//     excl[t][b] + rank in tile, where sub_pre = exclusive prefix of the
+//     sub-array histogram over x (known before the pass) and excl = the
+//     sum of b-counts of earlier tiles of the same sub-array, found by a
+//     look-back over status granules: status[t][b] = {tag, value} in one
+//     8-byte word, tag = 2*epoch + 1 for an inclusive prefix, 2*epoch for the
+//     tile's own count ("aggregate"), anything else = not yet published.
+//     A granule is written by one agent-scope store and polled with relaxed
+//     agent-scope loads (the guide's R2 form: the data is the flag, no
+//     fences).  The epoch is new every launch, so status needs no reset.
+//   * NEXT: the pass also accumulates the sub-array histogram of the next
+//     digit over its OUTPUT positions (the next pass's sub-arrays), in LDS,
+//     one add per record, flushed with global atomics at the end.
+// The first pass of a sort takes its sub-array histogram (and the key span)
+// from k_subhist: one read per sort instead of one per pass.
+constexpr int kSub = kOnesweepSubs;
+constexpr uint32_t kSpinLimit = 1u << 22;  // look-back polls before giving up (seconds)
+
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) uint32_t gu32;
+
+__device__ __forceinline__ int64_t sub_first_tile(int x, int64_t TT) { return (int64_t)x * TT / kSub; }
+__device__ __forceinline__ int sub_of_tile(int64_t t, int64_t TT) { return (int)((8 * t + 7) / TT); }
+
+// sub_hist[x * 256 + b] += number of records of sub-array x with digit b;
+// SPAN as in k_upsweep.  Workgroup c walks tiles [c*tpw, (c+1)*tpw).
+template <int BLOCK, int IPT, bool SPAN>
+__global__ __launch_bounds__(BLOCK) void k_subhist(const Elem* __restrict__ A, int64_t m,
+                                                   int shift, int64_t tiles_per_wg,
+                                                   uint32_t* __restrict__ sub_hist,
+                                                   unsigned long long* __restrict__ span) {
+  constexpr int W = BLOCK / 64;
+  constexpr int T = BLOCK * IPT;
+  __shared__ uint32_t hist[W][kBuckets];
+  __shared__ uint64_t span_or[W], span_nor[W];
+  uint64_t kor = 0, knor = 0;
+  for (int i = threadIdx.x; i < W * kBuckets; i += BLOCK) (&hist[0][0])[i] = 0;
+  const int w = threadIdx.x >> 6;
+  const int64_t TT = (m + T - 1) / T;
+  const int64_t t0 = (int64_t)blockIdx.x * tiles_per_wg;
+  const int64_t t1 = t0 + tiles_per_wg < TT ? t0 + tiles_per_wg : TT;
+  const uint64_t* __restrict__ keys = reinterpret_cast<const uint64_t*>(A);
+  int cur = t0 < t1 ? sub_of_tile(t0, TT) : 0;
+  __syncthreads();
+
+  auto flush = [&](int x) {
+    __syncthreads();
+    for (int b = threadIdx.x; b < kBuckets; b += BLOCK) {
+      uint32_t s = 0;
+#pragma unroll
+      for (int ww = 0; ww < W; ++ww) {
+        s += hist[ww][b];
+        hist[ww][b] = 0;
+      }
+      if (s) atomicAdd(&sub_hist[x * kBuckets + b], s);
+    }
+    __syncthreads();
+  };
+
+  for (int64_t tile = t0; tile < t1; ++tile) {
+    const int x = sub_of_tile(tile, TT);
+    if (x != cur) {
+      flush(cur);
+      cur = x;
+    }
+    const int64_t tb = tile * T;
+    const int64_t end = tb + T < m ? tb + T : m;
+    uint64_t k[IPT];
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+      const int64_t idx = tb + (int64_t)i * BLOCK + threadIdx.x;
+      k[i] = idx < end ? keys[2 * idx] : 0ull;
+    }
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+      const int64_t idx = tb + (int64_t)i * BLOCK + threadIdx.x;
+      const bool valid = idx < end;
+      if (SPAN && valid) {
+        kor |= k[i];
+        knor |= ~k[i];
+      }
+      const uint32_t d = (uint32_t)(k[i] >> shift) & (kBuckets - 1);
+      const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
+      if (__all(valid && d == d0)) {
+        if (lane_id() == 0) atomicAdd(&hist[w][d0], 64u);
+      } else if (valid) {
+        atomicAdd(&hist[w][d], 1u);
+      }
+    }
+  }
+  if (t0 < t1) flush(cur);
+  if (SPAN) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      kor |= __shfl_xor(kor, off, 64);
+      knor |= __shfl_xor(knor, off, 64);
+    }
+    if (lane_id() == 0) {
+      span_or[w] = kor;
+      span_nor[w] = knor;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint64_t o = 0, no = 0;
+#pragma unroll
+      for (int ww = 0; ww < W; ++ww) {
+        o |= span_or[ww];
+        no |= span_nor[ww];
+      }
+      atomicOr(&span[0], (unsigned long long)o);
+      atomicOr(&span[1], (unsigned long long)no);
+    }
+  }
+}
+
+__device__ __forceinline__ void store_granule(unsigned long long* p, uint32_t tag, uint32_t value) {
+  __hip_atomic_store((gu64*)p, ((unsigned long long)tag << 32) | value, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ unsigned long long load_granule(const unsigned long long* p) {
+  return __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int BLOCK, int IPT, bool NEXT>
+__global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
+    const Elem* __restrict__ in, Elem* __restrict__ out, int64_t m, int shift, int next_shift,
+    const uint32_t* __restrict__ sub_hist, uint32_t* __restrict__ next_hist,
+    unsigned long long* __restrict__ status, uint32_t* __restrict__ tile_ctr, uint32_t epoch,
+    uint32_t* __restrict__ err) {
+  constexpr int W = BLOCK / 64;
+  constexpr int T = BLOCK * IPT;
+  static_assert(BLOCK == kBuckets, "one thread per bucket in the look-back");
+
+  __shared__ Elem stage[T];                     // the ranked tile (64 KiB)
+  __shared__ uint32_t wcnt[W][kBuckets];        // per-wave digit counters -> positions
+  __shared__ int64_t delta[kBuckets];           // global dest = delta[digit] + tile position
+  __shared__ uint32_t cut[NEXT ? kBuckets : 1];  // next-pass sub-array of a run: see below
+  __shared__ uint32_t nh[NEXT ? kSub * kBuckets : 1];  // next digit's sub-array histogram
+  __shared__ uint64_t scan64[W];
+  __shared__ uint32_t scan32[W];
+  __shared__ int32_t s_tile, s_sub;
+
+  const int t = threadIdx.x;
+  const int w = t >> 6;
+  const uint32_t lane = lane_id();
+  const int64_t TT = (m + T - 1) / T;
+  const uint32_t tag_agg = 2u * epoch, tag_pre = 2u * epoch + 1u;
+
+  // Bucket starts (exclusive scan of the digit totals) and this thread's
+  // bucket column of the sub-array histogram.
+  uint32_t col[kSub];
+  uint64_t tot = 0;
+#pragma unroll
+  for (int x = 0; x < kSub; ++x) {
+    col[x] = sub_hist[x * kBuckets + t];
+    tot += col[x];
+  }
+  uint64_t all;
+  const uint64_t bstart = block_exclusive_scan<BLOCK>(tot, scan64, &all);
+  if (NEXT)
+    for (int i = t; i < kSub * kBuckets; i += BLOCK) nh[i] = 0;
+
+  int sub = (int)(blockIdx.x % kSub);  // thread 0's dequeue cursor
+  int tries = 0;
+  int cur_sub = -1;
+  uint64_t base = 0;  // bstart + sub_pre[cur_sub][t]
+
+  for (;;) {
+    if (t == 0) {
+      int tile = -1;
+      while (tries < kSub) {
+        const int64_t f0 = sub_first_tile(sub, TT), f1 = sub_first_tile(sub + 1, TT);
+        if (f1 > f0) {
+          const uint32_t j = atomicAdd(&tile_ctr[sub], 1u);
+          if ((int64_t)j < f1 - f0) {
+            tile = (int)(f0 + j);
+            break;
+          }
+        }
+        sub = sub + 1 == kSub ? 0 : sub + 1;
+        ++tries;
+      }
+      s_tile = tile;
+      s_sub = sub;
+    }
+#pragma unroll
+    for (int j = 0; j < kBuckets / 64; ++j) wcnt[w][lane + 64 * j] = 0;
+    __syncthreads();
+    const int tile = s_tile;
+    if (tile < 0) break;
+    const int x = s_sub;
+    if (x != cur_sub) {
+      cur_sub = x;
+      uint64_t pre = 0;
+#pragma unroll
+      for (int xx = 0; xx < kSub; ++xx) pre += xx < x ? col[xx] : 0u;
+      base = bstart + pre;
+    }
+    const int64_t tb = (int64_t)tile * T;
+    const int nvalid = (int)((m - tb) < T ? (m - tb) : T);
+
+    Elem e[IPT];
+    const int wbase = w * 64 * IPT + (int)lane;
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+      const int li = wbase + i * 64;
+      e[i] = li < nvalid ? load_elem(in + tb + li) : Elem{0ull, 0ull};
+    }
+    uint32_t rk[IPT];
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+      const bool valid = wbase + i * 64 < nvalid;
+      const uint32_t d = (uint32_t)(e[i].key >> shift) & (kBuckets - 1);
+      const uint64_t mt = match_digit8(d, __ballot(valid));
+      const uint32_t below = mbcnt(mt);
+      const uint32_t pre = wcnt[w][d];
+      rk[i] = pre + below;
+      if (valid && below == 0) wcnt[w][d] = pre + (uint32_t)__popcll(mt);
+    }
+    __syncthreads();
+
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int ww = 0; ww < W; ++ww) {
+      const uint32_t v = wcnt[ww][t];
+      wcnt[ww][t] = cnt;
+      cnt += v;
+    }
+    // Publish this tile's count of bucket t, then look back for the sum of
+    // the earlier tiles of the sub-array (the sub-array's first tile has none).
+    unsigned long long* my = status + (int64_t)tile * kBuckets + t;
+    uint64_t excl = 0;
+    if (tile == sub_first_tile(x, TT)) {
+      store_granule(my, tag_pre, cnt);
+    } else {
+      store_granule(my, tag_agg, cnt);
+      int64_t j = tile - 1;
+      uint32_t spins = 0;
+      bool done = false;
+      while (!done) {
+        const unsigned long long g = load_granule(status + j * kBuckets + t);
+        const uint32_t tag = (uint32_t)(g >> 32);
+        if (tag == tag_pre || tag == tag_agg) {
+          excl += (uint32_t)g;
+          if (tag == tag_pre) done = true;
+          else --j;
+        } else {
+          __builtin_amdgcn_s_sleep(1);
+          if ((++spins & 1023u) == 0 &&
+              (spins > kSpinLimit ||
+               __hip_atomic_load((gu32*)err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)) {
+            atomicOr(err, 1u);
+            done = true;
+          }
+        }
+      }
+      store_granule(my, tag_pre, (uint32_t)(excl + cnt));
+    }
+    uint32_t tile_total;
+    const uint32_t lstart = block_exclusive_scan<BLOCK>(cnt, scan32, &tile_total);
+    const int64_t R = (int64_t)(base + excl);  // first output slot of the run
+#pragma unroll
+    for (int ww = 0; ww < W; ++ww) wcnt[ww][t] += lstart;
+    delta[t] = R - (int64_t)lstart;
+    if (NEXT) {
+      // The run [R, R + cnt) lies in next-pass sub-array x0, except from
+      // stage position jb on (x1) when it crosses a sub-array boundary (at
+      // most one: a non-empty sub-array holds >= kTile records).
+      uint32_t c = 0xFFFFu;  // jb = 0xFFFF: never
+      if (cnt > 0) {
+        const int x0 = sub_of_tile(R / T, TT);
+        const int64_t bnd = x0 + 1 < kSub ? sub_first_tile(x0 + 1, TT) * T : m;
+        if (R + cnt > bnd) {
+          const int x1 = sub_of_tile(bnd / T, TT);
+          c = (uint32_t)(lstart + (bnd - R)) | ((uint32_t)x0 << 16) | ((uint32_t)x1 << 24);
+        } else {
+          c = 0xFFFFu | ((uint32_t)x0 << 16) | ((uint32_t)x0 << 24);
+        }
+      }
+      cut[t] = c;
+    }
+    __syncthreads();
+
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+      if (wbase + i * 64 < nvalid) {
+        const uint32_t d = (uint32_t)(e[i].key >> shift) & (kBuckets - 1);
+        stage[wcnt[w][d] + rk[i]] = e[i];
+      }
+    }
+    __syncthreads();
+
+    for (int j = t; j < nvalid; j += BLOCK) {
+      const Elem v = stage[j];
+      const uint32_t d = (uint32_t)(v.key >> shift) & (kBuckets - 1);
+      const int64_t g = delta[d] + j;
+      LSB_DASSERT(g >= 0 && g < m);
+      store_elem(out + g, v);
+      if (NEXT) {
+        const uint32_t c = cut[d];
+        const uint32_t xs = (uint32_t)j >= (c & 0xFFFFu) ? (c >> 24) : ((c >> 16) & 0xFFu);
+        const uint32_t dn = (uint32_t)(v.key >> next_shift) & (kBuckets - 1);
+        atomicAdd(&nh[xs * kBuckets + dn], 1u);
+      }
+    }
+    __syncthreads();
+  }
+  if (NEXT) {
+    for (int i = t; i < kSub * kBuckets; i += BLOCK)
+      if (nh[i]) atomicAdd(&next_hist[i], nh[i]);
+  }
+}
+
 // ------------------------------------------------------------------- place
 constexpr int kPlaceBlock = 256;
 constexpr int kPlaceIpt = 8;
@@ -952,6 +1280,52 @@ hipError_t launch_scatter(const Elem* in, Elem* out, int64_t m, int shift, Chunk
     hipLaunchKernelGGL((k_scatter<kScatterBlock, kScatterIpt, false>), dim3(ch.num_chunks),
                        dim3(kScatterBlock), 0, s, in, out, m, shift, ch.chunk_elems, ch.num_chunks,
                        chunk_off, totals, nullptr);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_subhist(const Elem* A, int64_t m, int shift, int grid, uint32_t* sub_hist,
+                          uint64_t* span, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(sub_hist, 0, sizeof(uint32_t) * kSub * kBuckets, s);
+  if (e != hipSuccess || m <= 0) return e;
+  const int64_t TT = (m + kTile - 1) / kTile;
+  if (grid < 1) grid = 1;
+  const int64_t tpw = (TT + grid - 1) / grid;
+  const dim3 g((unsigned)((TT + tpw - 1) / tpw));
+  if (span)
+    hipLaunchKernelGGL((k_subhist<kScatterBlock, kScatterIpt, true>), g, dim3(kScatterBlock), 0, s,
+                       A, m, shift, tpw, sub_hist, reinterpret_cast<unsigned long long*>(span));
+  else
+    hipLaunchKernelGGL((k_subhist<kScatterBlock, kScatterIpt, false>), g, dim3(kScatterBlock), 0, s,
+                       A, m, shift, tpw, sub_hist, nullptr);
+  return hipGetLastError();
+}
+
+hipError_t launch_onesweep(const Elem* in, Elem* out, int64_t m, int shift, int next_shift,
+                           const uint32_t* sub_hist, uint32_t* next_hist, uint64_t* status,
+                           uint32_t* tile_ctr, uint32_t epoch, uint32_t* err, int grid,
+                           hipStream_t s) {
+  if (m <= 0) return hipSuccess;
+  if (m > kOnesweepMaxElems || epoch == 0 || epoch >= (1u << 31) || shift < 0 || shift > 56 ||
+      next_shift > 56)
+    return hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(tile_ctr, 0, sizeof(uint32_t) * kSub, s);
+  if (e != hipSuccess) return e;
+  const int64_t TT = (m + kTile - 1) / kTile;
+  // Persistent grid, a multiple of the XCD count; no more than the tiles.
+  int64_t g = grid < kSub ? kSub : grid;
+  if (g > (TT + kSub - 1) / kSub * kSub) g = (TT + kSub - 1) / kSub * kSub;
+  auto* st = reinterpret_cast<unsigned long long*>(status);
+  if (next_shift >= 0) {
+    e = hipMemsetAsync(next_hist, 0, sizeof(uint32_t) * kSub * kBuckets, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((k_onesweep<kScatterBlock, kScatterIpt, true>), dim3((unsigned)g),
+                       dim3(kScatterBlock), 0, s, in, out, m, shift, next_shift, sub_hist,
+                       next_hist, st, tile_ctr, epoch, err);
+  } else {
+    hipLaunchKernelGGL((k_onesweep<kScatterBlock, kScatterIpt, false>), dim3((unsigned)g),
+                       dim3(kScatterBlock), 0, s, in, out, m, shift, 0, sub_hist, nullptr, st,
+                       tile_ctr, epoch, err);
   }
   return hipGetLastError();
 }

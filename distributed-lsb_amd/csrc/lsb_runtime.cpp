@@ -87,6 +87,13 @@ struct Rank {
   std::vector<Elem*> peer0, peer1;
   std::vector<void*> ipc_opened;
   int64_t* peer_base = nullptr;         // [nb]
+  // Single-read passes (LSB_OPT_ONESWEEP, P == 1), allocated on first use.
+  uint64_t* os_status = nullptr;        // [tiles][256] look-back granules
+  uint32_t* os_hist = nullptr;          // [2][8][256] sub-array histograms (ping-pong)
+  uint32_t* os_ctr = nullptr;           // [8] tile counters, [8] look-back error word
+  uint32_t* os_err_h = nullptr;         // pinned mirror of the error word
+  uint32_t os_epoch = 0;                // last look-back epoch
+  int os_grid = 0;                      // persistent grid (2 workgroups per CU)
   std::vector<int64_t> send_counts, send_displs, recv_counts, recv_displs;
 };
 
@@ -110,6 +117,7 @@ struct lsb_ctx {
   bool p2p = false;           // RCCL exchange as grouped ncclSend/ncclRecv, not ncclAllToAllv
   bool peer = false;          // exchange by direct stores into the owners' buffers
   bool peer_ready = false;    // peer tables set up
+  bool onesweep = true;       // P == 1: single-read passes (k_subhist + k_onesweep)
   // What the last lsb_sort ran (lsb_get_last_sort).
   int last_local_passes = 0;
   int last_exchanges = 0;
@@ -289,6 +297,10 @@ void free_rank(Rank& r) {
   }
   for (void* p : r.ipc_opened) (void)hipIpcCloseMemHandle(p);
   (void)hipFree(r.peer_base);
+  (void)hipFree(r.os_status);
+  (void)hipFree(r.os_hist);
+  (void)hipFree(r.os_ctr);
+  (void)hipHostFree(r.os_err_h);
   (void)hipFree(r.A);
   (void)hipFree(r.B);
   (void)hipFree(r.R);
@@ -776,6 +788,85 @@ int do_pass(lsb_ctx* c, int digit, uint64_t varying = ~0ull, bool want_span = fa
   return exchange_loopback(c, digit);
 }
 
+// ---- single-read passes (P == 1) ------------------------------------------
+bool onesweep_applies(const lsb_ctx* c) {
+  return c->onesweep && !exchanging(c) && c->ranks.size() == 1 && c->ranks[0].here > 0 &&
+         c->ranks[0].here <= lsb::kOnesweepMaxElems;
+}
+
+int onesweep_ensure(Rank& r) {
+  if (r.os_status) return LSB_OK;
+  const size_t tiles = (size_t)lsb::onesweep_tiles(r.here);
+  LSB_TRY(dev_alloc(&r.os_status, tiles * lsb::kBuckets));
+  LSB_TRY(dev_alloc(&r.os_hist, 2 * lsb::kOnesweepSubs * lsb::kBuckets));
+  LSB_TRY(dev_alloc(&r.os_ctr, 2 * lsb::kOnesweepSubs));
+  LSB_TRY(host_alloc(&r.os_err_h, 1));
+  *r.os_err_h = 0;
+  HIP_TRY(hipMemsetAsync(r.os_status, 0, tiles * lsb::kBuckets * sizeof(uint64_t), r.stream));
+  HIP_TRY(hipMemsetAsync(r.os_ctr, 0, 2 * lsb::kOnesweepSubs * sizeof(uint32_t), r.stream));
+  r.os_epoch = 0;
+  r.os_grid = max_chunks_for_device(r.dev);
+  return LSB_OK;
+}
+
+// lsb_sort when nothing is exchanged: one k_subhist read (digit 0's
+// sub-array histogram and the key span), then one k_onesweep per digit that
+// varies, each also counting the next such digit over its output.  Same
+// passes, same output as the reduce-then-scan loop (do_pass).
+int sort_onesweep(lsb_ctx* c) {
+  Rank& r = c->ranks[0];
+  HIP_TRY(hipSetDevice(r.dev));
+  LSB_TRY(onesweep_ensure(r));
+  const int64_t m = r.here;
+  uint32_t* hist[2] = {r.os_hist, r.os_hist + lsb::kOnesweepSubs * lsb::kBuckets};
+  HIP_TRY(hipMemsetAsync(r.span, 0, 2 * sizeof(uint64_t), r.stream));
+  {
+    Timer t(c, &r, LSB_K_UPSWEEP);
+    HIP_TRY(lsb::launch_subhist(r.A, m, 0, r.os_grid, hist[0], c->skip_constant ? r.span : nullptr,
+                                r.stream));
+  }
+  std::vector<int> digits{0};
+  if (c->skip_constant) {
+    HIP_TRY(hipMemcpyAsync(r.span_h, r.span, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, r.stream));
+    HIP_TRY(hipStreamSynchronize(r.stream));
+    c->last_varying = r.span_h[0] & r.span_h[1];
+  }
+  for (int d = 1; d < 64 / lsb::kDigitBits; ++d)
+    if (((c->last_varying >> (d * lsb::kDigitBits)) & (lsb::kBuckets - 1)) != 0) digits.push_back(d);
+  for (size_t i = 0; i < digits.size(); ++i) {
+    const int shift = digits[i] * lsb::kDigitBits;
+    const int next = i + 1 < digits.size() ? digits[i + 1] * lsb::kDigitBits : -1;
+    if (++r.os_epoch >= (1u << 30)) {  // tags 2*epoch(+1) stay below 2^31; start over
+      HIP_TRY(hipMemsetAsync(r.os_status, 0,
+                             (size_t)lsb::onesweep_tiles(m) * lsb::kBuckets * sizeof(uint64_t),
+                             r.stream));
+      r.os_epoch = 1;
+    }
+    {
+      Timer t(c, &r, LSB_K_SCATTER);
+      HIP_TRY(lsb::launch_onesweep(r.A, r.B, m, shift, next, hist[i & 1], hist[(i + 1) & 1],
+                                   r.os_status, r.os_ctr, r.os_epoch,
+                                   r.os_ctr + lsb::kOnesweepSubs, r.os_grid, r.stream));
+      if (c->timing) c->scatter_elems += m;
+    }
+    std::swap(r.A, r.B);
+    ++c->last_local_passes;
+  }
+  // The look-back's give-up word, read by lsb_sync.
+  HIP_TRY(hipMemcpyAsync(r.os_err_h, r.os_ctr + lsb::kOnesweepSubs, sizeof(uint32_t),
+                         hipMemcpyDeviceToHost, r.stream));
+  return LSB_OK;
+}
+
+// After a stream sync: did a look-back give up?  (Never expected: every
+// tile's predecessors belong to running workgroups.)
+int onesweep_check(Rank& r) {
+  if (!r.os_err_h || *r.os_err_h == 0) return LSB_OK;
+  *r.os_err_h = 0;
+  HIP_TRY(hipMemset(r.os_ctr + lsb::kOnesweepSubs, 0, sizeof(uint32_t)));
+  return fail(LSB_ERR_HIP, "k_onesweep", "look-back timed out; output invalid");
+}
+
 int check_ctx(const lsb_ctx* c) {
   if (!c) return fail(LSB_ERR_INVALID, "lsb", "null context");
   return LSB_OK;
@@ -1007,6 +1098,9 @@ int lsb_set_option(lsb_ctx_t* c, int option, int64_t value) {
     case LSB_OPT_SKIP_CONSTANT_DIGITS:
       c->skip_constant = value != 0;
       return LSB_OK;
+    case LSB_OPT_ONESWEEP:
+      c->onesweep = value != 0;
+      return LSB_OK;
     case LSB_OPT_EXCHANGE_PEER:
       c->peer = value != 0;
       return LSB_OK;
@@ -1093,7 +1187,9 @@ int lsb_sort(lsb_ctx_t* c) {
   const int passes = 64 / c->bits;
   c->last_local_passes = c->last_exchanges = 0;
   c->last_varying = ~0ull;
-  if (!c->skip_constant) {
+  if (onesweep_applies(c)) {
+    LSB_TRY(sort_onesweep(c));
+  } else if (!c->skip_constant) {
     for (int d = 0; d < passes; ++d) LSB_TRY(do_pass(c, d));
   } else {
     for (Rank& r : c->ranks) {
@@ -1129,6 +1225,7 @@ int lsb_sync(lsb_ctx_t* c) {
   for (Rank& r : c->ranks) {
     HIP_TRY(hipSetDevice(r.dev));
     HIP_TRY(hipStreamSynchronize(r.stream));
+    LSB_TRY(onesweep_check(r));
   }
   return LSB_OK;
 }

@@ -47,6 +47,7 @@ K_UPSWEEP, K_SCAN, K_SCATTER, K_EXCHANGE, K_PLACE, K_SORT = range(6)
 KERNEL_NAMES = ("upsweep", "scan", "scatter", "exchange", "place", "sort")
 OPT_TIMING, OPT_FORCE_EXCHANGE, OPT_SKIP_CONSTANT_DIGITS, OPT_EXCHANGE_SLICES, OPT_EXCHANGE_P2P = 0, 1, 2, 3, 4
 OPT_EXCHANGE_PEER = 5
+OPT_ONESWEEP = 6
 
 
 class LsbError(RuntimeError):

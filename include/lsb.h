@@ -81,6 +81,11 @@ typedef struct lsb_ctx lsb_ctx_t;
                                       (shmem_putmem / MPI_Put form; IPC-mapped across
                                       processes); no receive buffer, no placement pass.
                                       Opt-in: set on every rank before the first sort. */
+#define LSB_OPT_ONESWEEP        6  /* 1 (default): lsb_sort on a context that exchanges
+                                      nothing (P == 1) reads each record once per pass:
+                                      offsets by decoupled look-back, histograms carried
+                                      from pass to pass; 0: reduce-then-scan (count, scan,
+                                      scatter) like every other pass */
 
 /* ---- geometry: DistributedArray::create (mpi/mpi_lsbsort.cpp:144-149) ---- */
 int64_t lsb_per_rank(int64_t n_total, int num_ranks);            /* ceil(n/P) */

@@ -372,13 +372,17 @@ def test_rccl_world_of_one(lsb_built, oracle_mod, digests, p2p):
         w.close()
 
 
-def test_kernel_stats(lsb_built):
+@pytest.mark.parametrize("onesweep", [1, 0])
+def test_kernel_stats(lsb_built, onesweep):
     with lsb_built.World(1 << 20, ranks=1) as w:
+        w.set_option(lsb_built.OPT_ONESWEEP, onesweep)
         w.generate()
         w.set_timing(True)
         w.my_sort()
         st = w.kernel_stats()
-        assert st["scatter"][0] == 8 and st["upsweep"][0] == 8 and st["sort"][0] == 1
+        # single-read passes: one count read per sort, not one per pass
+        counts = 1 if onesweep else 8
+        assert st["scatter"][0] == 8 and st["upsweep"][0] == counts and st["sort"][0] == 1
         assert st["scatter"][1] > 0
         assert w.scatter_elems() == 8 << 20
 
