@@ -195,7 +195,7 @@ def load_traffic(workload, kernel):
     try:
         with open(path) as f:
             d = json.load(f)
-        if d.get("workload") == workload and d.get("kernel", "k_scatter") == kernel:
+        if d.get("workload") == workload and d.get("kernel", "k_scatter").split("<")[0] == kernel:
             return d.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass

@@ -95,6 +95,10 @@ hipError_t launch_subhist(const Elem* A, int64_t m, int shift, int grid, uint32_
 // allocation; epoch >= 1, new for every launch).  next_shift >= 0: also
 // next_hist (zeroed here) = sub_hist of the digit at next_shift over out.
 // tile_ctr: kOnesweepSubs words of scratch; *err |= 1 if a look-back gave up.
+// -DLSB_OS_PROFILE builds: summed s_memtime ticks of k_onesweep's phases
+// (dequeue, load + rank, look-back + scan, stage, write, unused) over all
+// workgroups' thread 0; hipErrorNotSupported otherwise.
+hipError_t onesweep_profile(unsigned long long* out6, bool reset);
 hipError_t launch_onesweep(const Elem* in, Elem* out, int64_t m, int shift, int next_shift,
                            const uint32_t* sub_hist, uint32_t* next_hist, uint64_t* status,
                            uint32_t* tile_ctr, uint32_t epoch, uint32_t* err, int grid,

@@ -543,12 +543,31 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_scatter(const Elem* __re
 // from k_subhist: one read per sort instead of one per pass.
 constexpr int kSub = kOnesweepSubs;
 constexpr uint32_t kSpinLimit = 1u << 22;  // look-back polls before giving up (seconds)
+#ifndef LSB_LOOKBACK
+#define LSB_LOOKBACK 1
+#endif
+#ifndef LSB_OS_SLEEP
+#define LSB_OS_SLEEP 1
+#endif
+// Predecessor granules read per look-back round trip: 1 measured fastest
+// (2: +6 %, 4: +11 % sort time): extra 8-byte loads cost more
+// than the round trips they save.
+constexpr int kLookback = LSB_LOOKBACK;
 
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) uint32_t gu32;
 
 __device__ __forceinline__ int64_t sub_first_tile(int x, int64_t TT) { return (int64_t)x * TT / kSub; }
-__device__ __forceinline__ int sub_of_tile(int64_t t, int64_t TT) { return (int)((8 * t + 7) / TT); }
+// Sub-array of tile t = (8t + 7) / TT without a division: the number of
+// x in 1..7 with x * TT <= 8t + 7 (32-bit exact: TT < 2^22, see
+// kOnesweepMaxElems).
+__device__ __forceinline__ int sub_of_tile(int64_t t, int64_t TT) {
+  const uint32_t num = 8u * (uint32_t)t + 7u, tt = (uint32_t)TT;
+  int x = 0;
+#pragma unroll
+  for (int k = 1; k < kSub; ++k) x += num >= (uint32_t)k * tt ? 1 : 0;
+  return x;
+}
 
 // sub_hist[x * 256 + b] += number of records of sub-array x with digit b;
 // SPAN as in k_upsweep.  Workgroup c walks tiles [c*tpw, (c+1)*tpw).
@@ -650,6 +669,23 @@ __device__ __forceinline__ unsigned long long load_granule(const unsigned long l
   return __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Phase timing (profiling build, -DLSB_OS_PROFILE): thread 0 of every
+// workgroup adds s_memtime deltas between the barriers of a tile into
+// g_os_prof[phase]; the runtime prints them at lsb_destroy.
+#ifdef LSB_OS_PROFILE
+__device__ unsigned long long g_os_prof[8];
+#define OS_MARK(k)                                                       \
+  do {                                                                   \
+    if (t == 0) {                                                        \
+      const uint64_t now = __builtin_amdgcn_s_memtime();                 \
+      prof[k] += now - prof_last;                                        \
+      prof_last = now;                                                   \
+    }                                                                    \
+  } while (0)
+#else
+#define OS_MARK(k) ((void)0)
+#endif
+
 template <int BLOCK, int IPT, bool NEXT>
 __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
     const Elem* __restrict__ in, Elem* __restrict__ out, int64_t m, int shift, int next_shift,
@@ -689,6 +725,10 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
   if (NEXT)
     for (int i = t; i < kSub * kBuckets; i += BLOCK) nh[i] = 0;
 
+#ifdef LSB_OS_PROFILE
+  uint64_t prof[6] = {0, 0, 0, 0, 0, 0};
+  uint64_t prof_last = __builtin_amdgcn_s_memtime();
+#endif
   int sub = (int)(blockIdx.x % kSub);  // thread 0's dequeue cursor
   int tries = 0;
   int cur_sub = -1;
@@ -715,6 +755,7 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
 #pragma unroll
     for (int j = 0; j < kBuckets / 64; ++j) wcnt[w][lane + 64 * j] = 0;
     __syncthreads();
+    OS_MARK(0);  // dequeue
     const int tile = s_tile;
     if (tile < 0) break;
     const int x = s_sub;
@@ -735,6 +776,16 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
       const int li = wbase + i * 64;
       e[i] = li < nvalid ? load_elem(in + tb + li) : Elem{0ull, 0ull};
     }
+    unsigned long long* my = status + (int64_t)tile * kBuckets + t;
+    const int64_t first = sub_first_tile(x, TT);
+    const bool head = tile == first;
+    int64_t j = tile - 1;  // newest predecessor not yet summed
+    unsigned long long g[kLookback];
+    uint32_t cnt = 0, lstart;
+    // Stable rank of every element among the wave's elements of its digit
+    // (per-wave counters), then the tile's counts: publish the aggregate,
+    // put the first look-back window in flight, and scan and stage the tile
+    // in LDS (neither needs the global offset) while it travels.
     uint32_t rk[IPT];
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
@@ -747,49 +798,73 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
       if (valid && below == 0) wcnt[w][d] = pre + (uint32_t)__popcll(mt);
     }
     __syncthreads();
-
-    uint32_t cnt = 0;
+    OS_MARK(1);  // load + rank
 #pragma unroll
     for (int ww = 0; ww < W; ++ww) {
       const uint32_t v = wcnt[ww][t];
       wcnt[ww][t] = cnt;
       cnt += v;
     }
-    // Publish this tile's count of bucket t, then look back for the sum of
-    // the earlier tiles of the sub-array (the sub-array's first tile has none).
-    unsigned long long* my = status + (int64_t)tile * kBuckets + t;
+    store_granule(my, head ? tag_pre : tag_agg, cnt);
+#pragma unroll
+    for (int k = 0; k < kLookback; ++k)
+      g[k] = (!head && j - k >= first) ? load_granule(status + (j - k) * kBuckets + t) : 0ull;
+    {
+      uint32_t tile_total;
+      lstart = block_exclusive_scan<BLOCK>(cnt, scan32, &tile_total);
+#pragma unroll
+      for (int ww = 0; ww < W; ++ww) wcnt[ww][t] += lstart;
+    }
+    __syncthreads();
+    OS_MARK(2);  // publish + scan
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+      if (wbase + i * 64 < nvalid) {
+        const uint32_t d = (uint32_t)(e[i].key >> shift) & (kBuckets - 1);
+        stage[wcnt[w][d] + rk[i]] = e[i];
+      }
+    }
+
+    // Finish the look-back (kLookback predecessors per round trip).
     uint64_t excl = 0;
-    if (tile == sub_first_tile(x, TT)) {
-      store_granule(my, tag_pre, cnt);
-    } else {
-      store_granule(my, tag_agg, cnt);
-      int64_t j = tile - 1;
+    if (!head) {
       uint32_t spins = 0;
-      bool done = false;
-      while (!done) {
-        const unsigned long long g = load_granule(status + j * kBuckets + t);
-        const uint32_t tag = (uint32_t)(g >> 32);
-        if (tag == tag_pre || tag == tag_agg) {
-          excl += (uint32_t)g;
-          if (tag == tag_pre) done = true;
-          else --j;
-        } else {
-          __builtin_amdgcn_s_sleep(1);
+      for (;;) {
+        // Sum the window from the newest: aggregates until an inclusive
+        // prefix (done) or a granule not yet published (read again).
+        int used = 0;
+        bool stop = false, done = false;
+#pragma unroll
+        for (int k = 0; k < kLookback; ++k) {
+          if (!stop) {
+            const uint32_t tag = (uint32_t)(g[k] >> 32);
+            if (tag == tag_pre || tag == tag_agg) {
+              excl += (uint32_t)g[k];
+              ++used;
+              if (tag == tag_pre) stop = done = true;
+            } else {
+              stop = true;
+            }
+          }
+        }
+        if (done) break;
+        j -= used;
+        if (used == 0) {
+          __builtin_amdgcn_s_sleep(LSB_OS_SLEEP);
           if ((++spins & 1023u) == 0 &&
               (spins > kSpinLimit ||
                __hip_atomic_load((gu32*)err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)) {
             atomicOr(err, 1u);
-            done = true;
+            break;
           }
         }
+#pragma unroll
+        for (int k = 0; k < kLookback; ++k)
+          g[k] = j - k >= first ? load_granule(status + (j - k) * kBuckets + t) : 0ull;
       }
       store_granule(my, tag_pre, (uint32_t)(excl + cnt));
     }
-    uint32_t tile_total;
-    const uint32_t lstart = block_exclusive_scan<BLOCK>(cnt, scan32, &tile_total);
     const int64_t R = (int64_t)(base + excl);  // first output slot of the run
-#pragma unroll
-    for (int ww = 0; ww < W; ++ww) wcnt[ww][t] += lstart;
     delta[t] = R - (int64_t)lstart;
     if (NEXT) {
       // The run [R, R + cnt) lies in next-pass sub-array x0, except from
@@ -809,15 +884,7 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
       cut[t] = c;
     }
     __syncthreads();
-
-#pragma unroll
-    for (int i = 0; i < IPT; ++i) {
-      if (wbase + i * 64 < nvalid) {
-        const uint32_t d = (uint32_t)(e[i].key >> shift) & (kBuckets - 1);
-        stage[wcnt[w][d] + rk[i]] = e[i];
-      }
-    }
-    __syncthreads();
+    OS_MARK(3);  // stage + look-back
 
     for (int j = t; j < nvalid; j += BLOCK) {
       const Elem v = stage[j];
@@ -833,7 +900,12 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
       }
     }
     __syncthreads();
+    OS_MARK(4);  // write
   }
+#ifdef LSB_OS_PROFILE
+  if (t == 0)
+    for (int k = 0; k < 6; ++k) atomicAdd(&g_os_prof[k], (unsigned long long)prof[k]);
+#endif
   if (NEXT) {
     for (int i = t; i < kSub * kBuckets; i += BLOCK)
       if (nh[i]) atomicAdd(&next_hist[i], nh[i]);
@@ -1282,6 +1354,19 @@ hipError_t launch_scatter(const Elem* in, Elem* out, int64_t m, int shift, Chunk
                        chunk_off, totals, nullptr);
   }
   return hipGetLastError();
+}
+
+hipError_t onesweep_profile(unsigned long long* out6, bool reset) {
+#ifdef LSB_OS_PROFILE
+  hipError_t e = hipMemcpyFromSymbol(out6, HIP_SYMBOL(g_os_prof), 6 * sizeof(unsigned long long));
+  if (e != hipSuccess || !reset) return e;
+  const unsigned long long z[8] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_os_prof), z, sizeof z);
+#else
+  for (int k = 0; k < 6; ++k) out6[k] = 0;
+  (void)reset;
+  return hipErrorNotSupported;
+#endif
 }
 
 hipError_t launch_subhist(const Elem* A, int64_t m, int shift, int grid, uint32_t* sub_hist,

@@ -842,9 +842,18 @@ int sort_onesweep(lsb_ctx* c) {
                              r.stream));
       r.os_epoch = 1;
     }
+#ifdef LSB_OS_NONEXT  // experiment: every pass's histogram from its own read
+    if (i > 0) {
+      Timer t(c, &r, LSB_K_UPSWEEP);
+      HIP_TRY(lsb::launch_subhist(r.A, m, shift, r.os_grid, hist[i & 1], nullptr, r.stream));
+    }
+    const int next_used = -1;
+#else
+    const int next_used = next;
+#endif
     {
       Timer t(c, &r, LSB_K_SCATTER);
-      HIP_TRY(lsb::launch_onesweep(r.A, r.B, m, shift, next, hist[i & 1], hist[(i + 1) & 1],
+      HIP_TRY(lsb::launch_onesweep(r.A, r.B, m, shift, next_used, hist[i & 1], hist[(i + 1) & 1],
                                    r.os_status, r.os_ctr, r.os_epoch,
                                    r.os_ctr + lsb::kOnesweepSubs, r.os_grid, r.stream));
       if (c->timing) c->scatter_elems += m;
@@ -860,6 +869,17 @@ int sort_onesweep(lsb_ctx* c) {
 
 // After a stream sync: did a look-back give up?  (Never expected: every
 // tile's predecessors belong to running workgroups.)
+#ifdef LSB_OS_PROFILE
+void os_profile_report() {
+  unsigned long long p[6];
+  if (lsb::onesweep_profile(p, true) != hipSuccess) return;
+  const double tot = (double)(p[0] + p[1] + p[2] + p[3] + p[4]) + 1e-9;
+  fprintf(stderr,
+          "os_profile: dequeue %.4f rank %.4f scan %.4f stage+lookback %.4f write %.4f (ticks %.0f)\n",
+          p[0] / tot, p[1] / tot, p[2] / tot, p[3] / tot, p[4] / tot, tot);
+}
+#endif
+
 int onesweep_check(Rank& r) {
   if (!r.os_err_h || *r.os_err_h == 0) return LSB_OK;
   *r.os_err_h = 0;
@@ -1080,6 +1100,10 @@ int lsb_create_rank_ops(lsb_ctx_t** out, int64_t n_total, int num_ranks, int ran
 void lsb_destroy(lsb_ctx_t* c) {
   if (!c) return;
   (void)resolve_timing(c);
+#ifdef LSB_OS_PROFILE
+  (void)lsb_sync(c);
+  os_profile_report();
+#endif
   for (Rank& r : c->ranks) free_rank(r);
   for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
   if (c->comm) (void)ncclCommDestroy(c->comm);

@@ -1,0 +1,19 @@
+#!/usr/bin/env python3
+"""Median sort / scatter ms per build from gpurun_out/ab.log (tools/ab.sh)."""
+import collections
+import re
+import statistics
+import sys
+
+path = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/ab.log"
+sort, scat, lib = collections.defaultdict(list), collections.defaultdict(list), None
+for line in open(path):
+    if line.startswith("lib="):
+        lib = line.strip()[4:]
+    m = re.search(r"wall=([\d.]+)ms.*scatter=([\d.]+)ms", line)
+    if m and lib:
+        sort[lib].append(float(m.group(1)))
+        scat[lib].append(float(m.group(2)))
+for k in sort:
+    print(f"{k:32s} sort {statistics.median(sort[k]):7.2f} ms (min {min(sort[k]):.2f})  "
+          f"scatter {statistics.median(scat[k]):7.2f} ms  n={len(sort[k])}")

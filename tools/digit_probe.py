@@ -13,6 +13,8 @@ import lsbsort  # noqa: E402
 lg = int(sys.argv[1]) if len(sys.argv) > 1 else 30
 n = 1 << lg
 w = lsbsort.World(n, 1)
+# LSB_PASSES=reduce-scan: count + scan + scatter per pass instead of single-read passes
+w.set_option(lsbsort.OPT_ONESWEEP, 0 if os.environ.get("LSB_PASSES") == "reduce-scan" else 1)
 w.set_timing(True)
 names = ["upsweep", "scan", "scatter", "exchange", "place", "sort"]
 for rep in range(2):

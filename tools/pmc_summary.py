@@ -23,8 +23,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def short(name):
+    """Kernel base name: template instances (k_onesweep<256, 16, true> and
+    <..., false>) are one kernel, averaged over all their launches."""
     name = name.replace("(anonymous namespace)::", "").replace("void ", "")
-    return name.split("(")[0].replace("lsb::", "")
+    return name.split("(")[0].replace("lsb::", "").split("<")[0]
 
 
 def per_kernel(path, counter):
@@ -35,6 +37,15 @@ def per_kernel(path, counter):
     return {k: sum(v) / len(v) for k, v in agg.items()}
 
 
+def durations_of(stats_csv):
+    calls, ns = collections.Counter(), collections.Counter()
+    for r in csv.DictReader(open(stats_csv)):
+        k = short(r["Name"])
+        calls[k] += int(r["Calls"])
+        ns[k] += float(r["TotalDurationNs"])
+    return {k: {"calls": calls[k], "avg_ms": ns[k] / calls[k] / 1e6} for k in calls}
+
+
 def main(tag, prof=os.path.join(ROOT, "gpurun_out", "prof"),
          workload="configs[1]: sort of 2^30 16-byte records per GPU, 8-bit digits, 8 passes, 1 GPU(s)",
          elems=1 << 30):
@@ -42,8 +53,7 @@ def main(tag, prof=os.path.join(ROOT, "gpurun_out", "prof"),
     out_dir = os.path.join(ROOT, "profiles")
     os.makedirs(out_dir, exist_ok=True)
     shutil.copy(stats_csv, os.path.join(out_dir, f"{tag}_kernel_stats.csv"))
-    durations = {short(r["Name"]): {"calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6}
-                 for r in csv.DictReader(open(stats_csv))}
+    durations = durations_of(stats_csv)
     fetch = per_kernel(os.path.join(prof, "fetch", "run_counter_collection.csv"), "FETCH_SIZE")
     write = per_kernel(os.path.join(prof, "write", "run_counter_collection.csv"), "WRITE_SIZE")
     kernels = {}
