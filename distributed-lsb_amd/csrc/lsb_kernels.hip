@@ -530,12 +530,17 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_scatter(const Elem* __re
 //     excl[t][b] + rank in tile, where sub_pre = exclusive prefix of the
 //     sub-array histogram over x (known before the pass) and excl = the
 //     sum of b-counts of earlier tiles of the same sub-array, found by a
-//     look-back over status granules: status[t][b] = {tag, value} in one
+//     look-back over status granules: status[t][b] = {value, tag} in one
 //     8-byte word, tag = 2*epoch + 1 for an inclusive prefix, 2*epoch for the
 //     tile's own count ("aggregate"), anything else = not yet published.
-//     A granule is written by one agent-scope store and polled with relaxed
-//     agent-scope loads (the guide's R2 form: the data is the flag, no
-//     fences).  The epoch is new every launch, so status needs no reset.
+//     Buckets b, b+1 travel as one 16-byte write-through (sc1) buffer store,
+//     polled with 16-byte sc1 loads (the guide's R2 form: the data is the
+//     flag, no fences); each half carries its own tag and a pair is used
+//     only when both agree.  The epoch is new every launch, so status needs
+//     no reset.  The tile publishes its aggregate right after ranking and
+//     reads its predecessor while it scans and stages; one predecessor per
+//     round trip measured fastest (wider windows: +6 % at 2, +11 % at 4),
+//     and the next tile's id is fetched while this one's records are written.
 //   * NEXT: the pass also accumulates the sub-array histogram of the next
 //     digit over its OUTPUT positions (the next pass's sub-arrays), in LDS,
 //     one add per record, flushed with global atomics at the end.
@@ -543,19 +548,12 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_scatter(const Elem* __re
 // from k_subhist: one read per sort instead of one per pass.
 constexpr int kSub = kOnesweepSubs;
 constexpr uint32_t kSpinLimit = 1u << 22;  // look-back polls before giving up (seconds)
-#ifndef LSB_LOOKBACK
-#define LSB_LOOKBACK 1
-#endif
 #ifndef LSB_OS_SLEEP
 #define LSB_OS_SLEEP 1
 #endif
-// Predecessor granules read per look-back round trip: 1 measured fastest
-// (2: +6 %, 4: +11 % sort time): extra 8-byte loads cost more
-// than the round trips they save.
-constexpr int kLookback = LSB_LOOKBACK;
 
-typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) uint32_t gu32;
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ int64_t sub_first_tile(int x, int64_t TT) { return (int64_t)x * TT / kSub; }
 // Sub-array of tile t = (8t + 7) / TT without a division: the number of
@@ -660,15 +658,6 @@ __global__ __launch_bounds__(BLOCK) void k_subhist(const Elem* __restrict__ A, i
   }
 }
 
-__device__ __forceinline__ void store_granule(unsigned long long* p, uint32_t tag, uint32_t value) {
-  __hip_atomic_store((gu64*)p, ((unsigned long long)tag << 32) | value, __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ unsigned long long load_granule(const unsigned long long* p) {
-  return __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // Phase timing (profiling build, -DLSB_OS_PROFILE): thread 0 of every
 // workgroup adds s_memtime deltas between the barriers of a tile into
 // g_os_prof[phase]; the runtime prints them at lsb_destroy.
@@ -733,24 +722,34 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
   int tries = 0;
   int cur_sub = -1;
   uint64_t base = 0;  // bstart + sub_pre[cur_sub][t]
+  // Thread 0: the next tile of sub-array `sub` in order, else of the next
+  // sub-array (-1 when all are taken).
+  auto grab = [&](int& tile_out, int& sub_out) {
+    int tile = -1;
+    while (tries < kSub) {
+      const int64_t f0 = sub_first_tile(sub, TT), f1 = sub_first_tile(sub + 1, TT);
+      if (f1 > f0) {
+        const uint32_t jj = atomicAdd(&tile_ctr[sub], 1u);
+        if ((int64_t)jj < f1 - f0) {
+          tile = (int)(f0 + jj);
+          break;
+        }
+      }
+      sub = sub + 1 == kSub ? 0 : sub + 1;
+      ++tries;
+    }
+    tile_out = tile;
+    sub_out = sub;
+  };
+  // The next tile's id is fetched while this tile's records are written
+  // (a device-scope atomic is ~1 us under load; 3 % of the sort, measured).
+  int nxt_tile = -1, nxt_sub = 0;
+  if (t == 0) grab(nxt_tile, nxt_sub);
 
   for (;;) {
     if (t == 0) {
-      int tile = -1;
-      while (tries < kSub) {
-        const int64_t f0 = sub_first_tile(sub, TT), f1 = sub_first_tile(sub + 1, TT);
-        if (f1 > f0) {
-          const uint32_t j = atomicAdd(&tile_ctr[sub], 1u);
-          if ((int64_t)j < f1 - f0) {
-            tile = (int)(f0 + j);
-            break;
-          }
-        }
-        sub = sub + 1 == kSub ? 0 : sub + 1;
-        ++tries;
-      }
-      s_tile = tile;
-      s_sub = sub;
+      s_tile = nxt_tile;
+      s_sub = nxt_sub;
     }
 #pragma unroll
     for (int j = 0; j < kBuckets / 64; ++j) wcnt[w][lane + 64 * j] = 0;
@@ -776,11 +775,20 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
       const int li = wbase + i * 64;
       e[i] = li < nvalid ? load_elem(in + tb + li) : Elem{0ull, 0ull};
     }
-    unsigned long long* my = status + (int64_t)tile * kBuckets + t;
+    // Status rows of this sub-array through one buffer descriptor (byte
+    // offsets < 2^31); the even lane of a pair publishes and polls buckets
+    // t, t + 1 as one 16-byte sc1 access: two self-tagged 8-byte halves,
+    // written by one store, so a pair is consumed only when both tags agree.
     const int64_t first = sub_first_tile(x, TT);
+    const int64_t last = sub_first_tile(x + 1, TT);
     const bool head = tile == first;
-    int64_t j = tile - 1;  // newest predecessor not yet summed
-    unsigned long long g[kLookback];
+    const bool even = (lane & 1u) == 0;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        status + first * kBuckets, 0, (int)((last - first) * kBuckets * 8), 0x00020000);
+    constexpr uint32_t kRowBytes = kBuckets * 8;
+    const uint32_t my_off = (uint32_t)(tile - first) * kRowBytes + (uint32_t)t * 8u;
+    uint32_t prow = (uint32_t)(tile - first) - 1u;  // newest predecessor row not yet summed
+    v4u g = {0u, 0u, 0u, 0u};
     uint32_t cnt = 0, lstart;
     // Stable rank of every element among the wave's elements of its digit
     // (per-wave counters), then the tile's counts: publish the aggregate,
@@ -805,10 +813,12 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
       wcnt[ww][t] = cnt;
       cnt += v;
     }
-    store_granule(my, head ? tag_pre : tag_agg, cnt);
-#pragma unroll
-    for (int k = 0; k < kLookback; ++k)
-      g[k] = (!head && j - k >= first) ? load_granule(status + (j - k) * kBuckets + t) : 0ull;
+    const uint32_t cnt_b = __shfl_down(cnt, 1, 64);
+    if (even) {
+      const uint32_t tg = head ? tag_pre : tag_agg;
+      __builtin_amdgcn_raw_buffer_store_b128(v4u{cnt, tg, cnt_b, tg}, rs, my_off, 0, 16);
+      if (!head) g = __builtin_amdgcn_raw_buffer_load_b128(rs, prow * kRowBytes + (uint32_t)t * 8u, 0, 16);
+    }
     {
       uint32_t tile_total;
       lstart = block_exclusive_scan<BLOCK>(cnt, scan32, &tile_total);
@@ -825,31 +835,16 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
       }
     }
 
-    // Finish the look-back (kLookback predecessors per round trip).
-    uint64_t excl = 0;
-    if (!head) {
+    uint64_t ea = 0, eb = 0;
+    if (even && !head) {
       uint32_t spins = 0;
       for (;;) {
-        // Sum the window from the newest: aggregates until an inclusive
-        // prefix (done) or a granule not yet published (read again).
-        int used = 0;
-        bool stop = false, done = false;
-#pragma unroll
-        for (int k = 0; k < kLookback; ++k) {
-          if (!stop) {
-            const uint32_t tag = (uint32_t)(g[k] >> 32);
-            if (tag == tag_pre || tag == tag_agg) {
-              excl += (uint32_t)g[k];
-              ++used;
-              if (tag == tag_pre) stop = done = true;
-            } else {
-              stop = true;
-            }
-          }
-        }
-        if (done) break;
-        j -= used;
-        if (used == 0) {
+        if (g.y == g.w && (g.y == tag_pre || g.y == tag_agg)) {
+          ea += g.x;
+          eb += g.z;
+          if (g.y == tag_pre) break;
+          --prow;
+        } else {
           __builtin_amdgcn_s_sleep(LSB_OS_SLEEP);
           if ((++spins & 1023u) == 0 &&
               (spins > kSpinLimit ||
@@ -858,12 +853,13 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
             break;
           }
         }
-#pragma unroll
-        for (int k = 0; k < kLookback; ++k)
-          g[k] = j - k >= first ? load_granule(status + (j - k) * kBuckets + t) : 0ull;
+        g = __builtin_amdgcn_raw_buffer_load_b128(rs, prow * kRowBytes + (uint32_t)t * 8u, 0, 16);
       }
-      store_granule(my, tag_pre, (uint32_t)(excl + cnt));
+      __builtin_amdgcn_raw_buffer_store_b128(
+          v4u{(uint32_t)(ea + cnt), tag_pre, (uint32_t)(eb + cnt_b), tag_pre}, rs, my_off, 0, 16);
     }
+    const uint64_t eb_left = __shfl_up(eb, 1, 64);
+    const uint64_t excl = even ? ea : eb_left;
     const int64_t R = (int64_t)(base + excl);  // first output slot of the run
     delta[t] = R - (int64_t)lstart;
     if (NEXT) {
@@ -885,6 +881,7 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
     }
     __syncthreads();
     OS_MARK(3);  // stage + look-back
+    if (t == 0) grab(nxt_tile, nxt_sub);  // in flight during the writes
 
     for (int j = t; j < nvalid; j += BLOCK) {
       const Elem v = stage[j];
