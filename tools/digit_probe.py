@@ -11,6 +11,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 import lsbsort  # noqa: E402
 
 lg = int(sys.argv[1]) if len(sys.argv) > 1 else 30
+DIST = os.environ.get("LSB_DIST", "uniform")  # uniform | zipf
 n = 1 << lg
 w = lsbsort.World(n, 1)
 # LSB_PASSES=reduce-scan: count + scan + scatter per pass instead of single-read passes
@@ -18,10 +19,10 @@ w.set_option(lsbsort.OPT_ONESWEEP, 0 if os.environ.get("LSB_PASSES") == "reduce-
 w.set_timing(True)
 names = ["upsweep", "scan", "scatter", "exchange", "place", "sort"]
 for rep in range(2):
-    w.generate()
+    w.generate(DIST)
     w.my_sort()
     w.sync()
-    w.generate()
+    w.generate(DIST)
     w.reset_kernel_stats()
     t0 = time.perf_counter()
     w.my_sort()
