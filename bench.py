@@ -53,9 +53,10 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=1 << 27,
                     help="records the CPU baseline sorts (bounded sample)")
     ap.add_argument("--no-verify", action="store_true")
-    ap.add_argument("--radix-bits", type=int, default=0,
-                    help="exchange digit width: 8 or 16 (default: 8 on 1 GPU, 16 on >1 GPU; "
-                         "local passes are 8-bit either way)")
+    ap.add_argument("--radix-bits", type=int, default=0, choices=(0, 8, 16, 64),
+                    help="exchange digit width: 8 or 16 (one all-to-all per digit), or 64 (the "
+                         "whole key: local sort, ONE all-to-all, merge); default 8 on 1 GPU, 64 on "
+                         ">1 GPU; local passes are 8-bit either way")
     ap.add_argument("--dist", choices=("uniform", "zipf"), default="uniform")
     ap.add_argument("--transport", choices=("rccl", "gloo"), default="rccl",
                     help="N > 1 collectives: RCCL over xGMI (the measurement), or gloo host "
@@ -235,6 +236,21 @@ def cpu_baseline(sample):
             "sample": f"oracle/lsb_oracle.c oracle_mpi_sort n={n} P=1 16-bit"}
 
 
+def parallelism(N, radix, a):
+    if N == 1:
+        return "1 GPU, no exchange"
+    if a.transport != "rccl":
+        return f"{N} ranks, gloo host collectives (rehearsal, not a measurement)"
+    if radix == 64:
+        return (f"block partition over {N} GPUs; local sort per GPU, splitter search (8 RCCL AllGathers "
+                f"of candidate counts), one RCCL " + ("AllToAllv" if a.exchange == "alltoallv" else
+                                                       "grouped Send/Recv") +
+                ", stable merge tree of the P runs")
+    return (f"block partition over {N} GPUs; per exchange digit RCCL AllGather of counts + " +
+            {"alltoallv": "AllToAllv in 4 slices", "p2p": "grouped Send/Recv in 4 slices",
+             "peer": "direct peer stores (IPC)"}[a.exchange])
+
+
 def main():
     a = parse()
     d = Dist()
@@ -242,7 +258,9 @@ def main():
     if d.world > 1 and a.gpus != d.world:
         N = d.world
     n_total = a.n_per_gpu * N
-    radix = a.radix_bits or (8 if N == 1 else 16)
+    radix = a.radix_bits or (8 if N == 1 else 64)
+    if radix == 64 and a.exchange == "peer":
+        raise SystemExit("--exchange peer is a per-digit exchange form; use --radix-bits 8 or 16")
     device = d.local_rank
     if d.world > 1 and a.transport == "gloo":
         # Rehearsal: ranks may share GPUs; collectives go through gloo on the host.
@@ -263,7 +281,9 @@ def main():
     elif a.exchange == "peer":
         w.set_option(lsbsort.OPT_EXCHANGE_PEER, 1)
     w.set_option(lsbsort.OPT_ONESWEEP, 1 if a.passes == "onesweep" else 0)
-    kernel = "k_onesweep" if (N == 1 and a.passes == "onesweep") else "k_scatter"
+    # Dominant kernel: the local pass.  Single-read passes run wherever a rank
+    # sorts its block alone: P = 1, and every rank of the whole-key exchange.
+    kernel = "k_onesweep" if ((N == 1 or radix == 64) and a.passes == "onesweep") else "k_scatter"
 
     def step(timed):
         w.generate(a.dist, a.zipf_s)
@@ -307,7 +327,9 @@ def main():
     else:
         cfg = "configs[2]" if a.dist == "uniform" else "configs[3]"
         workload = (f"{cfg}: sort of {N} x {size} 16-byte records block-partitioned over {N} GPUs, "
-                    f"8-bit local passes, {radix}-bit exchange digits ({64 // radix} all-to-alls)")
+                    f"8-bit local passes, " +
+                    (f"{radix}-bit exchange digits ({64 // radix} all-to-alls)" if radix != 64 else
+                     "whole-key exchange digit (local sort, 1 all-to-all, merge of the P runs)"))
     if a.dist != "uniform":
         workload += f", zipf s={a.zipf_s} keys"
     if m != 1 << 30:
@@ -347,7 +369,7 @@ def main():
                    "pass_form": ("single-read (k_subhist once, k_onesweep per pass)" if kernel == "k_onesweep"
                                  else "reduce-then-scan (k_upsweep, k_scan, k_scatter per pass)"), "exchange_digit_bits": radix if N > 1 else None,
                    "record_bytes": 16, "dist": a.dist,
-                   "parallelism": (f"block partition over {N} GPU(s); per exchange digit RCCL AllGather of counts + " + {"alltoallv": "AllToAllv in 4 slices", "p2p": "grouped Send/Recv in 4 slices", "peer": "direct peer stores (IPC)"}[a.exchange] if a.transport == "rccl" else f"{N} ranks, gloo host collectives (rehearsal, not a measurement)") if N > 1 else "1 GPU, no exchange"},
+                   "parallelism": parallelism(N, radix, a)},
         "roofline": roof,
         "sort_hbm_frac": round(sort_gbs / HBM_PEAK_GBS, 4),
         "kernel_ms_per_step": {k: round(v[1] / a.steps, 3) for k, v in stats.items()},

@@ -128,6 +128,30 @@ hipError_t launch_peer_exchange(const Elem* src, int64_t m, int shift, int nbuck
 hipError_t launch_plan(const uint64_t* hist, int P, int nb, int me, int64_t n, int64_t* work,
                        int64_t* total, int64_t* place, int64_t* counts, hipStream_t s);
 
+// ---- whole-key exchange (radix_bits = 64; lsb_merge.hip) ----
+// Splitter search: for Q targets T_t, state[2t .. 2t+1] = key interval
+// [lo, hi] holding the key found at global position T_t.  One round:
+// launch_split_cands (cnt[t * kSplitCands + j] = this rank's count of keys
+// below candidate j), all-gather cnt over the P ranks, launch_split_update.
+// kSplitRounds rounds leave lo == hi; launch_split_final then writes this
+// rank's {#keys < k*, #keys <= k*} per target.  A is sorted by key.
+constexpr int kSplitCands = 256;
+constexpr int kSplitRounds = 8;
+hipError_t launch_split_init(uint64_t* state, int Q, hipStream_t s);
+hipError_t launch_split_cands(const Elem* A, int64_t m, const uint64_t* state, int Q, uint64_t* cnt,
+                              hipStream_t s);
+hipError_t launch_split_update(const uint64_t* gathered, int P, int Q, const int64_t* targets,
+                               uint64_t* state, hipStream_t s);
+hipError_t launch_split_final(const Elem* A, int64_t m, const uint64_t* state, int Q, uint64_t* out,
+                              hipStream_t s);
+// Stable merge of two key-sorted runs (a before b on equal keys) into out
+// (na + nb records, disjoint from a and b).  path: merge_path_entries(na + nb)
+// int64 scratch; grid: persistent workgroups (4 per CU).
+constexpr int kMergeTile = 2048;
+inline int64_t merge_path_entries(int64_t n) { return (n + kMergeTile - 1) / kMergeTile + 1; }
+hipError_t launch_merge2(const Elem* a, int64_t na, const Elem* b, int64_t nb, Elem* out,
+                         int64_t* path, int grid, hipStream_t s);
+
 // O(n) bit-exact stable-sort check of a rank's here-part (see lsb_verify).
 // first_bad must hold UINT64_MAX before the launch; receives min bad global index.
 hipError_t launch_verify(const Elem* A, int64_t here, int64_t gbase, int64_t n, int64_t per,

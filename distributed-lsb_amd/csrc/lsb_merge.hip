@@ -1,0 +1,280 @@
+// Whole-key exchange (radix_bits = 64): the kernels of the one-exchange form
+// of the multi-GPU sort.
+//
+// With an exchange digit of 64 bits, globalShuffle (mpi/mpi_lsbsort.cpp:481-577)
+// has one pass: every rank sorts its block locally on the whole key (the
+// 8 stable 8-bit passes of localShuffle, :213-247), then the records move
+// once to the ranks owning their final global positions.  The order is the
+// reference's: key, then input position (rank, then local index), because the
+// local passes are stable and ranks are merged in rank order.
+//
+//   k_split_cands / k_split_update / k_split_final
+//       global position T_q = q * per (q = 1 .. P-1) -> the key k* found there
+//       and each rank's count of keys < k* and <= k*, by a 256-ary search of
+//       the key space (8 rounds for 64 bits; the per-candidate counts are
+//       binary searches in the rank's sorted block, summed over ranks from an
+//       all-gather).  This replaces copyCountsToGlobalCounts + exclusiveScan +
+//       copyStartsFromGlobalStarts (:327-479) for a digit with 2^64 buckets.
+//   k_merge_path / k_merge2
+//       the receiver's placement (:568-575): P sorted runs (one per source, in
+//       rank order) -> one sorted block, by a tree of stable two-way merges
+//       (ties: the left run, i.e. the lower source ranks, first).  Each merge
+//       is merge-path partitioned into 2048-output tiles staged in LDS and
+//       written back as whole, coalesced lines.
+#include "lsb_kernels.h"
+
+namespace lsb {
+namespace {
+
+__device__ __forceinline__ uint64_t key_at(const Elem* p, int64_t i) {
+  return reinterpret_cast<const uint64_t*>(p)[2 * i];
+}
+
+// #{i < m : A[i].key < k} (strict) or <= k, A sorted by key.
+template <bool kUpper>
+__device__ int64_t count_keys(const Elem* __restrict__ A, int64_t m, uint64_t k) {
+  int64_t lo = 0, hi = m;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    const uint64_t x = key_at(A, mid);
+    if (kUpper ? x <= k : x < k) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// Candidate j of the interval [lo, hi]: lo + j * step while inside, else hi.
+// step = width / 256 + 1, so the next interval is < step wide: 8 rounds take a
+// 64-bit interval to one key.  Nondecreasing in j.
+__device__ __forceinline__ uint64_t split_cand(uint64_t lo, uint64_t hi, int j) {
+  const uint64_t width = hi - lo;
+  const uint64_t step = (width >> 8) + 1;
+  const uint64_t off = (uint64_t)j * step;  // < 2^64: j < 256, step <= 2^56
+  return off <= width ? lo + off : hi;
+}
+
+// Thread (t, j): cnt[t * K + j] = #{keys < candidate j of target t}.
+__global__ __launch_bounds__(256) void k_split_cands(const Elem* __restrict__ A, int64_t m,
+                                                     const uint64_t* __restrict__ state, int Q,
+                                                     uint64_t* __restrict__ cnt) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= Q * kSplitCands) return;
+  const int t = i / kSplitCands, j = i % kSplitCands;
+  const uint64_t c = split_cand(state[2 * t], state[2 * t + 1], j);
+  cnt[i] = (uint64_t)count_keys<false>(A, m, c);
+}
+
+// One workgroup per target t: sum the P ranks' counts of every candidate,
+// keep the largest candidate with at most T_t keys below it (the key at
+// global position T_t is >= it) and cut the interval below the next one.
+__global__ __launch_bounds__(kSplitCands) void k_split_update(const uint64_t* __restrict__ gathered,
+                                                              int P, int Q,
+                                                              const int64_t* __restrict__ targets,
+                                                              uint64_t* __restrict__ state) {
+  __shared__ int best;
+  const int t = blockIdx.x, j = threadIdx.x;
+  const uint64_t lo = state[2 * t], hi = state[2 * t + 1];
+  uint64_t below = 0;
+  for (int s = 0; s < P; ++s) below += gathered[((size_t)s * Q + t) * kSplitCands + j];
+  if (j == 0) best = 0;
+  __syncthreads();
+  if (below <= (uint64_t)targets[t]) atomicMax(&best, j);
+  __syncthreads();
+  if (j == 0) {
+    const int b = best;
+    const uint64_t c = split_cand(lo, hi, b);
+    uint64_t nhi = hi;
+    if (b + 1 < kSplitCands) {
+      const uint64_t c1 = split_cand(lo, hi, b + 1);
+      if (c1 > c) nhi = c1 - 1;  // candidate b + 1 has more than T_t keys below it
+    }
+    state[2 * t] = c;
+    state[2 * t + 1] = nhi;
+  }
+}
+
+// out[2t] = #{keys < k*_t}, out[2t + 1] = #{keys <= k*_t} (k*_t = state lo).
+__global__ __launch_bounds__(64) void k_split_final(const Elem* __restrict__ A, int64_t m,
+                                                    const uint64_t* __restrict__ state, int Q,
+                                                    uint64_t* __restrict__ out) {
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= 2 * Q) return;
+  const uint64_t k = state[2 * (i >> 1)];
+  out[i] = (uint64_t)((i & 1) ? count_keys<true>(A, m, k) : count_keys<false>(A, m, k));
+}
+
+__global__ void k_split_init(uint64_t* __restrict__ state, int Q) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= Q) return;
+  state[2 * t] = 0;
+  state[2 * t + 1] = ~0ull;
+}
+
+// ------------------------------------------------------------------ merge
+// Stable merge of a (na) and b (nb): an a-record goes before an equal b-record.
+// Merge path: out[0, d) takes i records of a and d - i of b, with i the first
+// index where a[i] > b[d - 1 - i].
+__device__ __forceinline__ int64_t merge_path_global(const Elem* __restrict__ a, int64_t na,
+                                                     const Elem* __restrict__ b, int64_t nb,
+                                                     int64_t d) {
+  int64_t lo = d > nb ? d - nb : 0, hi = d < na ? d : na;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (key_at(a, mid) <= key_at(b, d - 1 - mid)) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// path[t] = co-rank (records of a) of output position min(t * kMergeTile, na + nb).
+__global__ __launch_bounds__(256) void k_merge_path(const Elem* __restrict__ a, int64_t na,
+                                                    const Elem* __restrict__ b, int64_t nb,
+                                                    int64_t tiles, int64_t* __restrict__ path) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t > tiles) return;
+  const int64_t n = na + nb;
+  const int64_t d = t * kMergeTile < n ? t * kMergeTile : n;
+  path[t] = merge_path_global(a, na, b, nb, d);
+}
+
+constexpr int kMergeBlock = 256;
+constexpr int kMergeIpt = kMergeTile / kMergeBlock;  // 8 outputs per thread
+
+// LDS slot of tile record x: one 16-byte pad slot after every 8 records.  A
+// thread's merge reads records ~4 apart from its neighbour's (8 outputs per
+// thread, half from each run); without the pad that stride puts many lanes
+// on the same banks.  Reads past a run's end are clamped (never used).
+__device__ __forceinline__ int merge_slot(int x) {
+  x = x < kMergeTile - 1 ? x : kMergeTile - 1;
+  return x + (x >> 3);
+}
+
+// Persistent: workgroup w merges tiles w, w + grid, ... (4 per CU, 40 KiB of
+// LDS each).  Per tile of kMergeTile outputs:
+//   1. its a- and b-ranges (from the tile path) -> LDS, 16-byte loads from
+//      consecutive lanes (a-range first, then the b-range);
+//   2. each thread owns kMergeIpt consecutive outputs: merge path inside the
+//      tile, then a sequential merge that writes the LDS slot of every output;
+//   3. output x of the tile = LDS record idx[x]: 16-byte stores from
+//      consecutive lanes, whole 128-byte lines.
+// tools/kbench/merge.hip: this shape runs at the speed of a plain copy of the
+// same bytes; one-shot 4096-record tiles (2 per CU) reach 2/3 of it, threads
+// storing their own outputs (lane-strided lines) 40 %.
+__global__ __launch_bounds__(kMergeBlock) void k_merge2(const Elem* __restrict__ a, int64_t na,
+                                                        const Elem* __restrict__ b, int64_t nb,
+                                                        const int64_t* __restrict__ path,
+                                                        int64_t tiles, Elem* __restrict__ out) {
+  __shared__ ulonglong2 tile[kMergeTile + kMergeTile / 8];   // 36 KiB
+  __shared__ uint16_t idx[kMergeTile];                       // 4 KiB
+  const int64_t n = na + nb;
+  const int t = threadIdx.x;
+  for (int64_t tt = blockIdx.x; tt < tiles; tt += gridDim.x) {
+    const int64_t d0 = tt * kMergeTile;
+    const int64_t d1 = d0 + kMergeTile < n ? d0 + kMergeTile : n;
+    const int64_t i0 = path[tt];
+    const int64_t j0 = d0 - i0;
+    const int ta = (int)(path[tt + 1] - i0);  // records of a in this tile
+    const int nt = (int)(d1 - d0);            // ta + tb
+    const int tb = nt - ta;
+
+    // 1. stage
+    {
+      ulonglong2 v[kMergeIpt];
+#pragma unroll
+      for (int k = 0; k < kMergeIpt; ++k) {
+        const int x = t + k * kMergeBlock;
+        if (x < nt) {
+          const Elem* p = x < ta ? a + (i0 + x) : b + (j0 + (x - ta));
+          v[k] = *reinterpret_cast<const ulonglong2*>(p);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < kMergeIpt; ++k) {
+        const int x = t + k * kMergeBlock;
+        if (x < nt) tile[merge_slot(x)] = v[k];
+      }
+    }
+    __syncthreads();
+
+    // 2. merge kMergeIpt outputs per thread
+    const int dl = t * kMergeIpt;
+    if (dl < nt) {
+      int lo = dl > tb ? dl - tb : 0, hi = dl < ta ? dl : ta;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (tile[merge_slot(mid)].x <= tile[merge_slot(ta + dl - 1 - mid)].x) lo = mid + 1;
+        else hi = mid;
+      }
+      int ia = lo, ib = dl - lo;
+      uint64_t ka = tile[merge_slot(ia)].x, kb = tile[merge_slot(ta + ib)].x;
+      const int end = dl + kMergeIpt < nt ? dl + kMergeIpt : nt;
+      for (int k = dl; k < end; ++k) {
+        const bool take_a = ib >= tb || (ia < ta && ka <= kb);
+        idx[k] = (uint16_t)merge_slot(take_a ? ia : ta + ib);
+        if (take_a) ++ia;
+        else ++ib;
+        const uint64_t nk = tile[merge_slot(take_a ? ia : ta + ib)].x;
+        if (take_a) ka = nk;
+        else kb = nk;
+      }
+    }
+    __syncthreads();
+
+    // 3. write out in output order
+#pragma unroll
+    for (int k = 0; k < kMergeIpt; ++k) {
+      const int x = t + k * kMergeBlock;
+      if (x < nt) *reinterpret_cast<ulonglong2*>(out + (d0 + x)) = tile[idx[x]];
+    }
+    __syncthreads();  // the tile's LDS is reused
+  }
+}
+
+}  // namespace
+
+hipError_t launch_split_init(uint64_t* state, int Q, hipStream_t s) {
+  if (Q <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_split_init, dim3((Q + 63) / 64), dim3(64), 0, s, state, Q);
+  return hipGetLastError();
+}
+
+hipError_t launch_split_cands(const Elem* A, int64_t m, const uint64_t* state, int Q, uint64_t* cnt,
+                              hipStream_t s) {
+  if (Q <= 0) return hipSuccess;
+  const int threads = Q * kSplitCands;
+  hipLaunchKernelGGL(k_split_cands, dim3((threads + 255) / 256), dim3(256), 0, s, A, m, state, Q,
+                     cnt);
+  return hipGetLastError();
+}
+
+hipError_t launch_split_update(const uint64_t* gathered, int P, int Q, const int64_t* targets,
+                               uint64_t* state, hipStream_t s) {
+  if (Q <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_split_update, dim3(Q), dim3(kSplitCands), 0, s, gathered, P, Q, targets,
+                     state);
+  return hipGetLastError();
+}
+
+hipError_t launch_split_final(const Elem* A, int64_t m, const uint64_t* state, int Q, uint64_t* out,
+                              hipStream_t s) {
+  if (Q <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_split_final, dim3((2 * Q + 63) / 64), dim3(64), 0, s, A, m, state, Q, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_merge2(const Elem* a, int64_t na, const Elem* b, int64_t nb, Elem* out,
+                         int64_t* path, int grid, hipStream_t s) {
+  const int64_t n = na + nb;
+  if (n == 0) return hipSuccess;
+  const int64_t tiles = (n + kMergeTile - 1) / kMergeTile;
+  hipLaunchKernelGGL(k_merge_path, dim3((unsigned)((tiles + 1 + 255) / 256)), dim3(256), 0, s, a,
+                     na, b, nb, tiles, path);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const int64_t g = tiles < grid ? tiles : grid;
+  hipLaunchKernelGGL(k_merge2, dim3((unsigned)g), dim3(kMergeBlock), 0, s, a, na, b, nb, path, tiles,
+                     out);
+  return hipGetLastError();
+}
+
+}  // namespace lsb

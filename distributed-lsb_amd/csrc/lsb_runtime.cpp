@@ -94,6 +94,15 @@ struct Rank {
   uint32_t* os_err_h = nullptr;         // pinned mirror of the error word
   uint32_t os_epoch = 0;                // last look-back epoch
   int os_grid = 0;                      // persistent grid (2 workgroups per CU)
+  // Whole-key exchange (radix_bits = 64), allocated on first use.
+  uint64_t* split_state = nullptr;      // [Q][2] key interval per target
+  int64_t* split_targets = nullptr;     // [Q] global positions q * per
+  uint64_t* split_cnt = nullptr;        // [Q][kSplitCands] counts below the candidates
+  uint64_t* split_gather = nullptr;     // [P][Q][kSplitCands] all-gathered
+  uint64_t* split_fin = nullptr;        // [Q][2] #keys < k*, #keys <= k*
+  uint64_t* split_fin_gather = nullptr; // [P][Q][2]
+  uint64_t* split_h = nullptr;          // pinned mirror of split_fin_gather
+  int64_t* merge_path = nullptr;        // merge-path tile boundaries
   std::vector<int64_t> send_counts, send_displs, recv_counts, recv_displs;
 };
 
@@ -104,8 +113,8 @@ struct lsb_ctx {
   int64_t n = 0;
   int64_t per = 0;
   int P = 1;
-  int bits = 8;      // exchange digit width: 8 or 16
-  int nb = 256;      // 1 << bits
+  int bits = 8;      // exchange digit width: 8, 16, or 64 (the whole key: one exchange)
+  int nb = 256;      // 1 << bits (256 for bits = 64: the buckets of the local passes)
   int first_rank = 0;
   std::vector<Rank> ranks;  // local ranks
   ncclComm_t comm = nullptr;
@@ -297,6 +306,14 @@ void free_rank(Rank& r) {
   }
   for (void* p : r.ipc_opened) (void)hipIpcCloseMemHandle(p);
   (void)hipFree(r.peer_base);
+  (void)hipFree(r.split_state);
+  (void)hipFree(r.split_targets);
+  (void)hipFree(r.split_cnt);
+  (void)hipFree(r.split_gather);
+  (void)hipFree(r.split_fin);
+  (void)hipFree(r.split_fin_gather);
+  (void)hipHostFree(r.split_h);
+  (void)hipFree(r.merge_path);
   (void)hipFree(r.os_status);
   (void)hipFree(r.os_hist);
   (void)hipFree(r.os_ctr);
@@ -770,7 +787,10 @@ int exchange_rccl(lsb_ctx* c, int digit) {
 // varying: key bits that differ somewhere; a sub-pass whose byte is constant
 // is the identity and is skipped (all ~0 = run everything).  want_span: the
 // first sub-pass also reduces the key span (lsb_sort, digit 0).
+int merge_sort(lsb_ctx* c);
+
 int do_pass(lsb_ctx* c, int digit, uint64_t varying = ~0ull, bool want_span = false) {
+  if (c->bits == 64 && exchanging(c)) return merge_sort(c);  // the one 64-bit digit
   for (Rank& r : c->ranks) r.starts_fused = false;
   const int subs = c->bits / lsb::kDigitBits;
   for (int sub = 0; sub < subs; ++sub) {
@@ -813,8 +833,9 @@ int onesweep_ensure(Rank& r) {
 // sub-array histogram and the key span), then one k_onesweep per digit that
 // varies, each also counting the next such digit over its output.  Same
 // passes, same output as the reduce-then-scan loop (do_pass).
-int sort_onesweep(lsb_ctx* c) {
-  Rank& r = c->ranks[0];
+// Rank r alone (its local block); *passes gets the passes it ran, *varying the
+// key bits that vary in the block.
+int sort_onesweep_rank(lsb_ctx* c, Rank& r, int* passes, uint64_t* varying) {
   HIP_TRY(hipSetDevice(r.dev));
   LSB_TRY(onesweep_ensure(r));
   const int64_t m = r.here;
@@ -826,13 +847,15 @@ int sort_onesweep(lsb_ctx* c) {
                                 r.stream));
   }
   std::vector<int> digits{0};
+  *varying = ~0ull;
+  *passes = 0;
   if (c->skip_constant) {
     HIP_TRY(hipMemcpyAsync(r.span_h, r.span, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, r.stream));
     HIP_TRY(hipStreamSynchronize(r.stream));
-    c->last_varying = r.span_h[0] & r.span_h[1];
+    *varying = r.span_h[0] & r.span_h[1];
   }
   for (int d = 1; d < 64 / lsb::kDigitBits; ++d)
-    if (((c->last_varying >> (d * lsb::kDigitBits)) & (lsb::kBuckets - 1)) != 0) digits.push_back(d);
+    if (((*varying >> (d * lsb::kDigitBits)) & (lsb::kBuckets - 1)) != 0) digits.push_back(d);
   for (size_t i = 0; i < digits.size(); ++i) {
     const int shift = digits[i] * lsb::kDigitBits;
     const int next = i + 1 < digits.size() ? digits[i + 1] * lsb::kDigitBits : -1;
@@ -859,12 +882,287 @@ int sort_onesweep(lsb_ctx* c) {
       if (c->timing) c->scatter_elems += m;
     }
     std::swap(r.A, r.B);
-    ++c->last_local_passes;
+    ++*passes;
   }
   // The look-back's give-up word, read by lsb_sync.
   HIP_TRY(hipMemcpyAsync(r.os_err_h, r.os_ctr + lsb::kOnesweepSubs, sizeof(uint32_t),
                          hipMemcpyDeviceToHost, r.stream));
   return LSB_OK;
+}
+
+int sort_onesweep(lsb_ctx* c) {
+  return sort_onesweep_rank(c, c->ranks[0], &c->last_local_passes, &c->last_varying);
+}
+
+// ---- whole-key exchange (radix_bits = 64) ----------------------------------
+// globalShuffle with a 64-bit digit (mpi/mpi_lsbsort.cpp:481-577 with one
+// pass): each rank sorts its block locally on the whole key, the ranks find
+// where the global positions q * per fall (a splitter search over the sorted
+// blocks, in place of the count transposes and scan of :327-479), every rank
+// sends each owner one contiguous range (one all-to-all-v for the whole sort,
+// :316-324), and each owner merges its P sorted runs in rank order (the
+// placement of :568-575).  Same output as 64 / 8 or 64 / 16 exchanges: the
+// stable order by key, ties by input position.
+
+// Targets of the splitter search: global positions T_q = q * per for
+// q = 1 .. Q, the q with q * per < n (beyond n a source sends everything
+// below, so its cut is its whole block).
+int merge_targets(const lsb_ctx* c) {
+  int Q = 0;
+  while (Q + 1 < c->P && (int64_t)(Q + 1) * c->per < c->n) ++Q;
+  return Q;
+}
+
+// Host side of the plan: from every rank's {#keys < k*_q, #keys <= k*_q}
+// (fin[(s * Q + q - 1) * 2 + {0,1}]) the cut of source s at T_q is
+//   below_s + min(equal_s, max(0, T_q - sum_s below_s - sum_{s' < s} equal_s'))
+// (equal keys in rank order = input order), and
+//   send to q:  my cuts [q, q + 1);  receive from s: s's cuts [me, me + 1).
+int plan_merge_core(int64_t n, int P, int me, int Q, const uint64_t* fin, int64_t* sc, int64_t* sd,
+                    int64_t* rc, int64_t* rd) {
+  const int64_t per = div_ceil(n, P);
+  // cut[s * (P + 1) + q], q = 0 .. P
+  std::vector<int64_t> cut((size_t)P * (P + 1));
+  for (int s = 0; s < P; ++s) {
+    cut[(size_t)s * (P + 1)] = 0;
+    for (int q = 1; q <= P; ++q) cut[(size_t)s * (P + 1) + q] = here_of(n, P, s);
+  }
+  for (int q = 1; q <= Q; ++q) {
+    const int64_t T = (int64_t)q * per;
+    int64_t below = 0, all = 0;
+    for (int s = 0; s < P; ++s) {
+      const uint64_t b = fin[((size_t)s * Q + q - 1) * 2], u = fin[((size_t)s * Q + q - 1) * 2 + 1];
+      if (b > u || (int64_t)u > here_of(n, P, s))
+        return fail(LSB_ERR_INVALID, "plan_merge", "counts out of range");
+      below += (int64_t)b;
+      all += (int64_t)u;
+    }
+    if (!(below <= T && T < all)) return fail(LSB_ERR_INVALID, "plan_merge", "target not bracketed");
+    int64_t rem = T - below;
+    for (int s = 0; s < P; ++s) {
+      const int64_t b = (int64_t)fin[((size_t)s * Q + q - 1) * 2];
+      const int64_t eq = (int64_t)fin[((size_t)s * Q + q - 1) * 2 + 1] - b;
+      const int64_t take = std::min(eq, rem);
+      cut[(size_t)s * (P + 1) + q] = b + take;
+      rem -= take;
+    }
+  }
+  int64_t a = 0, b = 0;
+  for (int q = 0; q < P; ++q) {
+    sc[q] = cut[(size_t)me * (P + 1) + q + 1] - cut[(size_t)me * (P + 1) + q];
+    rc[q] = cut[(size_t)q * (P + 1) + me + 1] - cut[(size_t)q * (P + 1) + me];
+    if (sc[q] < 0 || rc[q] < 0) return fail(LSB_ERR_INVALID, "plan_merge", "cuts not monotone");
+    sd[q] = a;
+    rd[q] = b;
+    a += sc[q];
+    b += rc[q];
+  }
+  if (b != here_of(n, P, me)) return fail(LSB_ERR_INVALID, "plan_merge", "receive total");
+  return LSB_OK;
+}
+
+int merge_ensure(lsb_ctx* c, Rank& r, int Q) {
+  HIP_TRY(hipSetDevice(r.dev));
+  if (!r.R) LSB_TRY(dev_alloc(&r.R, (size_t)c->per));
+  if (!r.merge_path) LSB_TRY(dev_alloc(&r.merge_path, (size_t)lsb::merge_path_entries(c->per)));
+  if (r.split_state || Q == 0) return LSB_OK;
+  const size_t P = (size_t)c->P, K = lsb::kSplitCands;
+  LSB_TRY(dev_alloc(&r.split_state, 2 * (size_t)Q));
+  LSB_TRY(dev_alloc(&r.split_targets, (size_t)Q));
+  LSB_TRY(dev_alloc(&r.split_cnt, (size_t)Q * K));
+  LSB_TRY(dev_alloc(&r.split_gather, P * Q * K));
+  LSB_TRY(dev_alloc(&r.split_fin, 2 * (size_t)Q));
+  LSB_TRY(dev_alloc(&r.split_fin_gather, P * 2 * Q));
+  LSB_TRY(host_alloc(&r.split_h, P * 2 * Q));
+  std::vector<int64_t> t(Q);
+  for (int q = 1; q <= Q; ++q) t[q - 1] = (int64_t)q * c->per;
+  HIP_TRY(hipMemcpy(r.split_targets, t.data(), sizeof(int64_t) * Q, hipMemcpyHostToDevice));
+  return LSB_OK;
+}
+
+// recv[s * count ..] = send of rank s, for every local rank (loopback: device
+// copies once every rank's stream is done; otherwise the collective).
+template <typename SendOf, typename RecvOf>
+int gather_ranks(lsb_ctx* c, size_t count, SendOf send_of, RecvOf recv_of) {
+  if (c->mode != Mode::kLoopback) {
+    Rank& r = c->ranks[0];
+    HIP_TRY(hipSetDevice(r.dev));
+    return coll_allgather_u64(c, r, send_of(r), recv_of(r), count);
+  }
+  for (Rank& r : c->ranks) {
+    HIP_TRY(hipSetDevice(r.dev));
+    HIP_TRY(hipStreamSynchronize(r.stream));
+  }
+  for (Rank& q : c->ranks) {
+    HIP_TRY(hipSetDevice(q.dev));
+    for (Rank& s : c->ranks)
+      HIP_TRY(hipMemcpyAsync(recv_of(q) + (size_t)s.rank * count, send_of(s), count * 8,
+                             hipMemcpyDefault, q.stream));
+  }
+  return LSB_OK;
+}
+
+// Rank r's block sorted on the whole key: single-read passes, or count + scan
+// + scatter when they do not apply.  Digits constant over the block are skipped.
+int sort_local_rank(lsb_ctx* c, Rank& r, int* passes, uint64_t* varying) {
+  *passes = 0;
+  *varying = 0;
+  if (r.here == 0) return LSB_OK;
+  if (c->onesweep && r.here <= lsb::kOnesweepMaxElems) return sort_onesweep_rank(c, r, passes, varying);
+  HIP_TRY(hipSetDevice(r.dev));
+  HIP_TRY(hipMemsetAsync(r.span, 0, 2 * sizeof(uint64_t), r.stream));
+  LSB_TRY(local_pass(c, r, 0, c->skip_constant));
+  *passes = 1;
+  *varying = ~0ull;
+  if (c->skip_constant) {
+    HIP_TRY(hipMemcpyAsync(r.span_h, r.span, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, r.stream));
+    HIP_TRY(hipStreamSynchronize(r.stream));
+    *varying = r.span_h[0] & r.span_h[1];
+  }
+  for (int d = 1; d < 64 / lsb::kDigitBits; ++d) {
+    if (((*varying >> (d * lsb::kDigitBits)) & (lsb::kBuckets - 1)) == 0) continue;
+    LSB_TRY(local_pass(c, r, d * lsb::kDigitBits));
+    ++*passes;
+  }
+  return LSB_OK;
+}
+
+// The owner's P sorted runs (source order) -> one sorted block in A: a tree
+// of stable two-way merges, adjacent runs paired so the lower ranks stay on
+// the left.  Level k writes B (k even) or A (k odd); a run without a partner
+// is copied.  Ends with the block in A (swapped in if it landed in B).
+int merge_runs(lsb_ctx* c, Rank& r) {
+  struct Run {
+    const Elem* p;
+    int64_t n;
+  };
+  std::vector<Run> runs;
+  for (int s = 0; s < c->P; ++s) {
+    if (r.recv_counts[s] == 0) continue;
+    runs.push_back({s == r.rank ? r.A + r.send_displs[s] : r.R + r.recv_displs[s], r.recv_counts[s]});
+  }
+  if (runs.empty() || (runs.size() == 1 && runs[0].p == r.A)) return LSB_OK;
+  HIP_TRY(hipSetDevice(r.dev));
+  Timer t(c, &r, LSB_K_PLACE);
+  int level = 0;
+  while (runs.size() > 1 || level == 0) {
+    Elem* dst = (level % 2 == 0) ? r.B : r.A;
+    std::vector<Run> next;
+    int64_t off = 0;
+    for (size_t i = 0; i < runs.size(); i += 2) {
+      if (i + 1 < runs.size()) {
+        HIP_TRY(lsb::launch_merge2(runs[i].p, runs[i].n, runs[i + 1].p, runs[i + 1].n, dst + off,
+                                   r.merge_path, 2 * max_chunks_for_device(r.dev), r.stream));
+        next.push_back({dst + off, runs[i].n + runs[i + 1].n});
+      } else {
+        HIP_TRY(hipMemcpyAsync(dst + off, runs[i].p, (size_t)runs[i].n * sizeof(Elem),
+                               hipMemcpyDeviceToDevice, r.stream));
+        next.push_back({dst + off, runs[i].n});
+      }
+      off += next.back().n;
+    }
+    runs.swap(next);
+    ++level;
+  }
+  if (level % 2 == 1) std::swap(r.A, r.B);  // the last level wrote B
+  return LSB_OK;
+}
+
+int exchange_merge(lsb_ctx* c) {
+  const int P = c->P;
+  const int Q = merge_targets(c);
+  const size_t K = lsb::kSplitCands;
+  for (Rank& r : c->ranks) LSB_TRY(merge_ensure(c, r, Q));
+  // 1. splitter search: kSplitRounds rounds of candidate counts, all-gathered.
+  if (Q > 0) {
+    for (Rank& r : c->ranks) {
+      HIP_TRY(hipSetDevice(r.dev));
+      HIP_TRY(lsb::launch_split_init(r.split_state, Q, r.stream));
+    }
+    for (int round = 0; round < lsb::kSplitRounds; ++round) {
+      for (Rank& r : c->ranks) {
+        HIP_TRY(hipSetDevice(r.dev));
+        Timer t(c, &r, LSB_K_EXCHANGE);
+        HIP_TRY(lsb::launch_split_cands(r.A, r.here, r.split_state, Q, r.split_cnt, r.stream));
+      }
+      LSB_TRY(gather_ranks(c, (size_t)Q * K, [](Rank& r) { return r.split_cnt; },
+                           [](Rank& r) { return r.split_gather; }));
+      for (Rank& r : c->ranks) {
+        HIP_TRY(hipSetDevice(r.dev));
+        HIP_TRY(lsb::launch_split_update(r.split_gather, P, Q, r.split_targets, r.split_state,
+                                         r.stream));
+      }
+    }
+    for (Rank& r : c->ranks) {
+      HIP_TRY(hipSetDevice(r.dev));
+      HIP_TRY(lsb::launch_split_final(r.A, r.here, r.split_state, Q, r.split_fin, r.stream));
+    }
+    LSB_TRY(gather_ranks(c, 2 * (size_t)Q, [](Rank& r) { return r.split_fin; },
+                         [](Rank& r) { return r.split_fin_gather; }));
+    for (Rank& r : c->ranks) {
+      HIP_TRY(hipSetDevice(r.dev));
+      HIP_TRY(hipMemcpyAsync(r.split_h, r.split_fin_gather, sizeof(uint64_t) * P * 2 * Q,
+                             hipMemcpyDeviceToHost, r.stream));
+    }
+  }
+  // 2. the plan, on the host (the all-to-all takes host counts)
+  for (Rank& r : c->ranks) {
+    HIP_TRY(hipSetDevice(r.dev));
+    HIP_TRY(hipStreamSynchronize(r.stream));
+    LSB_TRY(plan_merge_core(c->n, P, r.rank, Q, r.split_h, r.send_counts.data(),
+                            r.send_displs.data(), r.recv_counts.data(), r.recv_displs.data()));
+  }
+  // 3. one all-to-all-v of contiguous ranges (the self range stays in A)
+  if (c->mode == Mode::kLoopback) {
+    for (Rank& q : c->ranks) {
+      HIP_TRY(hipSetDevice(q.dev));
+      Timer t(c, &q, LSB_K_EXCHANGE);
+      for (Rank& s : c->ranks) {
+        if (s.rank == q.rank || s.send_counts[q.rank] == 0) continue;
+        if (s.send_counts[q.rank] != q.recv_counts[s.rank])
+          return fail(LSB_ERR_STATE, "exchange_merge", "send/recv count mismatch");
+        HIP_TRY(hipMemcpyAsync(q.R + q.recv_displs[s.rank], s.A + s.send_displs[q.rank],
+                               (size_t)q.recv_counts[s.rank] * sizeof(Elem), hipMemcpyDefault,
+                               q.stream));
+      }
+    }
+    // No rank's merge may overwrite its A while another rank still copies from it.
+    for (Rank& r : c->ranks) {
+      HIP_TRY(hipSetDevice(r.dev));
+      HIP_TRY(hipStreamSynchronize(r.stream));
+    }
+  } else {
+    Rank& r = c->ranks[0];
+    HIP_TRY(hipSetDevice(r.dev));
+    std::vector<size_t> sc(P), sd(P), rc(P), rdp(P);
+    for (int q = 0; q < P; ++q) {
+      sc[q] = q == r.rank ? 0 : (size_t)r.send_counts[q] * 2;
+      rc[q] = q == r.rank ? 0 : (size_t)r.recv_counts[q] * 2;
+      sd[q] = (size_t)r.send_displs[q] * 2;
+      rdp[q] = (size_t)r.recv_displs[q] * 2;
+    }
+    Timer t(c, &r, LSB_K_EXCHANGE);
+    LSB_TRY(coll_alltoallv_u64(c, r, reinterpret_cast<const uint64_t*>(r.A), sc.data(), sd.data(),
+                               reinterpret_cast<uint64_t*>(r.R), rc.data(), rdp.data()));
+  }
+  // 4. merge the runs
+  for (Rank& r : c->ranks) LSB_TRY(merge_runs(c, r));
+  return LSB_OK;
+}
+
+// lsb_sort / lsb_pass(0) with a 64-bit exchange digit on an exchanging context.
+int merge_sort(lsb_ctx* c) {
+  c->last_local_passes = 0;
+  c->last_varying = 0;
+  for (Rank& r : c->ranks) {
+    int passes = 0;
+    uint64_t varying = 0;
+    LSB_TRY(sort_local_rank(c, r, &passes, &varying));
+    c->last_local_passes = std::max(c->last_local_passes, passes);
+    c->last_varying |= varying;
+  }
+  c->last_exchanges = 1;
+  return exchange_merge(c);
 }
 
 // After a stream sync: did a look-back give up?  (Never expected: every
@@ -899,7 +1197,7 @@ lsb_ctx* new_ctx(int64_t n_total, int num_ranks, int radix_bits) {
   c->P = num_ranks;
   c->per = div_ceil(n_total, num_ranks);
   c->bits = radix_bits;
-  c->nb = 1 << radix_bits;
+  c->nb = radix_bits == 64 ? lsb::kBuckets : 1 << radix_bits;
   return c;
 }
 
@@ -1012,8 +1310,8 @@ int lsb_create(lsb_ctx_t** out, int64_t n_total, int num_ranks, const int* dev_i
   *out = nullptr;
   if (n_total < 0 || num_ranks < 1 || num_ranks > 64)
     return fail(LSB_ERR_INVALID, "lsb_create", "n or P");
-  if (radix_bits != 8 && radix_bits != 16)
-    return fail(LSB_ERR_UNSUPPORTED, "lsb_create", "radix_bits must be 8 or 16");
+  if (radix_bits != 8 && radix_bits != 16 && radix_bits != 64)
+    return fail(LSB_ERR_UNSUPPORTED, "lsb_create", "radix_bits must be 8, 16 or 64");
   lsb_ctx* c = new_ctx(n_total, num_ranks, radix_bits);
   if (!c) return LSB_ERR_NOMEM;
   c->mode = Mode::kLoopback;
@@ -1045,8 +1343,8 @@ int lsb_create_rank(lsb_ctx_t** out, int64_t n_total, int num_ranks, int rank, i
   *out = nullptr;
   if (n_total < 0 || num_ranks < 1 || num_ranks > 64 || rank < 0 || rank >= num_ranks || !id)
     return fail(LSB_ERR_INVALID, "lsb_create_rank", "n, P, rank or id");
-  if (radix_bits != 8 && radix_bits != 16)
-    return fail(LSB_ERR_UNSUPPORTED, "lsb_create_rank", "radix_bits must be 8 or 16");
+  if (radix_bits != 8 && radix_bits != 16 && radix_bits != 64)
+    return fail(LSB_ERR_UNSUPPORTED, "lsb_create_rank", "radix_bits must be 8, 16 or 64");
   lsb_ctx* c = new_ctx(n_total, num_ranks, radix_bits);
   if (!c) return LSB_ERR_NOMEM;
   c->mode = Mode::kRccl;
@@ -1080,8 +1378,8 @@ int lsb_create_rank_ops(lsb_ctx_t** out, int64_t n_total, int num_ranks, int ran
   if (n_total < 0 || num_ranks < 1 || num_ranks > 64 || rank < 0 || rank >= num_ranks || !ops ||
       !ops->allgather || !ops->alltoallv || !ops->allreduce_min_i64 || !ops->barrier)
     return fail(LSB_ERR_INVALID, "lsb_create_rank_ops", "n, P, rank or ops");
-  if (radix_bits != 8 && radix_bits != 16)
-    return fail(LSB_ERR_UNSUPPORTED, "lsb_create_rank_ops", "radix_bits must be 8 or 16");
+  if (radix_bits != 8 && radix_bits != 16 && radix_bits != 64)
+    return fail(LSB_ERR_UNSUPPORTED, "lsb_create_rank_ops", "radix_bits must be 8, 16 or 64");
   lsb_ctx* c = new_ctx(n_total, num_ranks, radix_bits);
   if (!c) return LSB_ERR_NOMEM;
   c->mode = Mode::kOps;
@@ -1211,7 +1509,9 @@ int lsb_sort(lsb_ctx_t* c) {
   const int passes = 64 / c->bits;
   c->last_local_passes = c->last_exchanges = 0;
   c->last_varying = ~0ull;
-  if (onesweep_applies(c)) {
+  if (c->bits == 64 && exchanging(c)) {
+    LSB_TRY(merge_sort(c));
+  } else if (onesweep_applies(c)) {
     LSB_TRY(sort_onesweep(c));
   } else if (!c->skip_constant) {
     for (int d = 0; d < passes; ++d) LSB_TRY(do_pass(c, d));
@@ -1402,6 +1702,29 @@ int lsb_plan_exchange_device(int dev, int64_t n_total, int P, int me, int nb, co
   (void)hipFree(d_place);
   (void)hipFree(d_counts);
   return rc;
+}
+
+int lsb_plan_merge(int64_t n_total, int P, int me, const int64_t* below, const int64_t* upto,
+                   int64_t* send_counts, int64_t* send_displs, int64_t* recv_counts,
+                   int64_t* recv_displs) {
+  if (P < 1 || P > 64 || me < 0 || me >= P || n_total < 0 || (P > 1 && (!below || !upto)) ||
+      !send_counts || !send_displs || !recv_counts || !recv_displs)
+    return fail(LSB_ERR_INVALID, "lsb_plan_merge", "arguments");
+  lsb_ctx c;
+  c.n = n_total;
+  c.P = P;
+  c.per = div_ceil(n_total, P);
+  const int Q = merge_targets(&c);
+  std::vector<uint64_t> fin((size_t)P * 2 * Q);
+  for (int s = 0; s < P; ++s)
+    for (int q = 0; q < Q; ++q) {
+      const int64_t b = below[(size_t)s * (P - 1) + q], u = upto[(size_t)s * (P - 1) + q];
+      if (b < 0 || u < 0) return fail(LSB_ERR_INVALID, "lsb_plan_merge", "negative count");
+      fin[((size_t)s * Q + q) * 2] = (uint64_t)b;
+      fin[((size_t)s * Q + q) * 2 + 1] = (uint64_t)u;
+    }
+  return plan_merge_core(n_total, P, me, Q, fin.data(), send_counts, send_displs, recv_counts,
+                         recv_displs);
 }
 
 int lsb_plan_exchange(int64_t n_total, int P, int me, int nb, const int64_t* hist,

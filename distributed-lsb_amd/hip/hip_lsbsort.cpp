@@ -14,7 +14,8 @@
 //              (default 0), exchange by device copies; same results as
 //              `mpirun -n P mpi_lsbsort` on one GPU.
 //   --json     also print one machine-readable line.
-//   --radix-bits 8|16   exchange digit width (local passes are always 8-bit)
+//   --radix-bits 8|16|64  exchange digit width (local passes are always 8-bit);
+//              64: local sort, one all-to-all, merge of the P runs
 //   --dist uniform|zipf [--zipf-s S]   key distribution of the same pcg64 stream
 //   --exchange alltoallv|p2p|peer  element exchange (default RCCL AllToAllv in
 //              slices; grouped Send/Recv; direct peer stores, the shmem_putmem form)

@@ -155,6 +155,7 @@ def _lib() -> ctypes.CDLL:
             "lsb_get_scatter_elems": (i32, [vp, P64]),
             "lsb_plan_exchange": (i32, [i64, i32, i32, i32, vp, vp, vp, vp, vp, vp]),
             "lsb_plan_exchange_device": (i32, [i32, i64, i32, i32, i32, vp, vp, vp, vp, vp, vp]),
+            "lsb_plan_merge": (i32, [i64, i32, i32, vp, vp, vp, vp, vp, vp]),
             "lsb_strerror": (cp, [i32]),
         }
         for name, (res, args) in sig.items():
@@ -201,6 +202,20 @@ def plan_exchange(n: int, P: int, rank: int, hist: np.ndarray, device: Optional[
         _check(_lib().lsb_plan_exchange(*args), "lsb_plan_exchange")
     else:
         _check(_lib().lsb_plan_exchange_device(device, *args), "lsb_plan_exchange_device")
+    return out
+
+
+def plan_merge(n: int, P: int, rank: int, below: np.ndarray, upto: np.ndarray) -> dict:
+    """Whole-key exchange plan of rank `rank` (lsb_plan_merge): below/upto are
+    P x (P-1) counts of keys <, <= the key at global position q * per."""
+    below = np.ascontiguousarray(below, dtype=np.int64).reshape(P, max(P - 1, 0))
+    upto = np.ascontiguousarray(upto, dtype=np.int64).reshape(P, max(P - 1, 0))
+    out = {k: np.zeros(P, dtype=np.int64) for k in
+           ("send_counts", "send_displs", "recv_counts", "recv_displs")}
+    _check(_lib().lsb_plan_merge(n, P, rank, below.ctypes.data, upto.ctypes.data,
+                                 out["send_counts"].ctypes.data, out["send_displs"].ctypes.data,
+                                 out["recv_counts"].ctypes.data, out["recv_displs"].ctypes.data),
+           "lsb_plan_merge")
     return out
 
 

@@ -98,7 +98,11 @@ int64_t lsb_here(int64_t n_total, int num_ranks, int rank);      /* clamp(n - r*
  * buckets, 8 passes) or 16 (65536 buckets, 4 passes: the reference's own
  * RADIX, mpi/mpi_lsbsort.cpp:21).  On device every digit is sorted by
  * stable 8-bit local passes (a 16-bit digit = low byte, then high byte), so
- * the output is the same for both; 16 halves the all-to-alls when P > 1. */
+ * the output is the same for both; 16 halves the all-to-alls when P > 1.
+ * radix_bits = 64 makes the whole key one digit: each rank sorts its block
+ * (all 8 local passes), then ONE all-to-all moves every record to its owner,
+ * which merges the P sorted runs in rank order (lsb_plan_merge).  Same
+ * output again; one exchange per sort instead of 64 / radix_bits. */
 int  lsb_create(lsb_ctx_t** ctx, int64_t n_total, int num_ranks,
                 const int* dev_ids, int radix_bits);
 /* RCCL bootstrap: rank 0 calls this and ships the bytes to the other ranks
@@ -216,6 +220,24 @@ int  lsb_plan_exchange_device(int dev_id, int64_t n_total, int num_ranks, int ra
                               int64_t* send_counts, int64_t* send_displs,
                               int64_t* recv_counts, int64_t* recv_displs,
                               int64_t* place_off);
+
+/* Plan of the whole-key exchange (radix_bits = 64), host side.  After every
+ * rank has sorted its block on the whole key, let k*_q be the key at global
+ * position T_q = q * per (q = 1 .. P-1, the q with T_q < n) and
+ *   below[s * (P-1) + q-1] = #records of rank s with key <  k*_q
+ *   upto [s * (P-1) + q-1] = #records of rank s with key <= k*_q
+ * (entries of targets T_q >= n are ignored).  Records of equal key keep rank
+ * order, so source s's cut at T_q is below + min(equal, what T_q still
+ * needs after the lower ranks).  Rank `rank` then sends its sorted range
+ * [cut_q, cut_{q+1}) to q and receives [cut_rank, cut_{rank+1}) of every s:
+ * counts and displacements (records) as for lsb_plan_exchange.  This is the
+ * rule the runtime applies to the all-gathered counts of its device splitter
+ * search (k_split_*), replacing copyCountsToGlobalCounts / exclusiveScan /
+ * copyStartsFromGlobalStarts (mpi/mpi_lsbsort.cpp:327-479) for a digit of
+ * 2^64 buckets.  LSB_ERR_INVALID when the counts do not bracket a target. */
+int  lsb_plan_merge(int64_t n_total, int num_ranks, int rank, const int64_t* below,
+                    const int64_t* upto, int64_t* send_counts, int64_t* send_displs,
+                    int64_t* recv_counts, int64_t* recv_displs);
 
 const char* lsb_strerror(int code);
 

@@ -229,3 +229,87 @@ def test_planner_rejects_bad_input(lsb_built):
     assert lib.lsb_plan_exchange(10, P, 0, nb, hist.ctypes.data, *ptrs) == 1   # negative count
     hist[0, 3] = 11
     assert lib.lsb_plan_exchange(10, P, 0, nb, hist.ctypes.data, *ptrs) == 1   # counts exceed n
+
+
+# ------------------------------------------------- whole-key exchange plan
+def simulate_merge(lsbsort, inp_parts, n, P):
+    """radix_bits = 64 on the CPU: every rank sorts its block (stable, by key),
+    the cuts come from lsb_plan_merge given each rank's counts below / up to
+    the key at global position q * per (derived here independently, from the
+    globally sorted keys), one all-to-all of contiguous ranges, then each
+    owner merges its P runs in rank order."""
+    per = -(-n // P) if P else 0
+    A = [x[np.argsort(x["key"], kind="stable")] for x in inp_parts]
+    allkeys = np.sort(np.concatenate([x["key"] for x in A])) if n else np.zeros(0, np.uint64)
+    below = np.zeros((P, max(P - 1, 0)), np.int64)
+    upto = np.zeros_like(below)
+    for q in range(1, P):
+        T = q * per
+        if T >= n:
+            continue
+        k = allkeys[T]
+        for s in range(P):
+            below[s, q - 1] = np.searchsorted(A[s]["key"], k, side="left")
+            upto[s, q - 1] = np.searchsorted(A[s]["key"], k, side="right")
+    plans = [lsbsort.plan_merge(n, P, r, below, upto) for r in range(P)]
+    out = []
+    for q in range(P):
+        runs = []
+        for s in range(P):
+            c = plans[s]["send_counts"][q]
+            assert c == plans[q]["recv_counts"][s]
+            so = plans[s]["send_displs"][q]
+            runs.append(A[s][so:so + c])
+        R = np.concatenate(runs)
+        assert R.size == lsbsort.here(n, P, q)
+        out.append(R[np.argsort(R["key"], kind="stable")])  # stable merge, rank order
+    return np.concatenate(out) if out else np.empty(0, inp_parts[0].dtype)
+
+
+def _parts(oracle, n, P, keymap=None):
+    per = -(-n // P)
+    slots = oracle.generate_slots(n, P)
+    parts = [slots[r * per: r * per + (max(0, min(per, n - r * per)))].copy() for r in range(P)]
+    if keymap is not None:
+        for x in parts:
+            x["key"] = keymap(x["key"])
+    return parts
+
+
+@pytest.mark.parametrize("row", [0, 1, 3, 4])
+def test_simulated_merge_exchange_reproduces_golden(lsb_built, oracle_mod, digests, row):
+    d = digests["rows"][row]
+    out = simulate_merge(lsb_built, _parts(oracle_mod, d["n"], d["P"]), d["n"], d["P"])
+    assert oracle_mod.digest(out) == d["output"]
+
+
+@pytest.mark.parametrize("n,P", [(0, 3), (1, 4), (5, 8), (17, 8), (1001, 7), (4096, 64)])
+def test_simulated_merge_exchange_small(lsb_built, oracle_mod, n, P):
+    out = simulate_merge(lsb_built, _parts(oracle_mod, n, P), n, P)
+    assert np.array_equal(out, oracle_mod.mpi_sort(n, P))
+
+
+@pytest.mark.parametrize("name,keymap", [
+    ("three_values", lambda k: k % np.uint64(3)),
+    ("all_equal", lambda k: np.zeros_like(k)),
+    ("hot_key", lambda k: np.where(k % np.uint64(4) == 0, np.uint64(7), k)),
+])
+@pytest.mark.parametrize("n,P", [(10_007, 2), (20_000, 5), (3_333, 8)])
+def test_simulated_merge_exchange_duplicates(lsb_built, oracle_mod, name, keymap, n, P):
+    """Equal keys straddling owner boundaries: cuts follow rank order."""
+    parts = _parts(oracle_mod, n, P, keymap)
+    out = simulate_merge(lsb_built, parts, n, P)
+    inp = np.concatenate(parts)
+    assert np.array_equal(out, inp[np.argsort(inp["key"], kind="stable")])
+
+
+def test_plan_merge_rejects_bad_counts(lsb_built):
+    n, P = 100, 2
+    ok = lsb_built.plan_merge(n, P, 0, np.array([[40], [9]]), np.array([[41], [10]]))
+    assert list(ok["send_counts"]) == [41, 9] and list(ok["recv_counts"]) == [41, 9]
+    with pytest.raises(lsb_built.LsbError):      # target 50 not bracketed
+        lsb_built.plan_merge(n, P, 0, np.array([[10], [10]]), np.array([[20], [20]]))
+    with pytest.raises(lsb_built.LsbError):      # below > upto
+        lsb_built.plan_merge(n, P, 0, np.array([[30], [30]]), np.array([[20], [40]]))
+    with pytest.raises(lsb_built.LsbError):      # more than the rank holds
+        lsb_built.plan_merge(n, P, 0, np.array([[40], [9]]), np.array([[60], [10]]))

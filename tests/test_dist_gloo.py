@@ -95,3 +95,93 @@ def test_world_size_2_reproduces_reference_digest(tmp_path, digests, oracle_mod)
                        join=True, start_method="spawn")
     out = np.concatenate([np.load(tmp_path / f"rank{r}.npy") for r in range(world)])
     assert oracle_mod.digest(out) == row["output"]
+
+
+# ------------------------------------------- whole-key exchange (radix 64)
+K = 256  # lsb::kSplitCands
+
+
+def _cand(lo, hi, j):
+    """split_cand (csrc/lsb_merge.hip): lo + j * step inside [lo, hi], else hi."""
+    width = hi - lo
+    off = j * ((width >> 8) + 1)
+    return lo + off if off <= width else hi
+
+
+def _merge_worker(rank, world, port, n, result_dir):
+    for p in (ROOT, os.path.join(ROOT, "distributed-lsb_amd"), os.path.join(ROOT, "oracle")):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import torch
+    import torch.distributed as dist
+    import lsbsort
+    import oracle
+    import bench
+
+    d = bench.Dist()
+    per, here = lsbsort.per_rank(n, world), lsbsort.here(n, world, rank)
+    A = oracle.generate_slots(n, world)[rank * per: rank * per + here].copy()
+    A = A[np.argsort(A["key"], kind="stable")]  # stands in for the 8 local single-read passes
+    keys = A["key"]
+    Q = sum(1 for q in range(1, world) if q * per < n)
+    lo, hi = [0] * Q, [2**64 - 1] * Q
+
+    def allgather(arr):
+        out = [torch.zeros_like(arr) for _ in range(world)]
+        dist.all_gather(out, arr)
+        return torch.stack(out).numpy()
+
+    for _ in range(8):  # kSplitRounds: k_split_cands -> all-gather -> k_split_update
+        cands = np.array([[_cand(lo[t], hi[t], j) for j in range(K)] for t in range(Q)], dtype=np.uint64)
+        cnt = np.searchsorted(keys, cands.ravel(), side="left").astype(np.int64).reshape(Q, K)
+        tot = allgather(torch.from_numpy(cnt)).sum(axis=0)
+        for t in range(Q):
+            b = max(j for j in range(K) if tot[t, j] <= (t + 1) * per)
+            c = _cand(lo[t], hi[t], b)
+            nhi = hi[t]
+            if b + 1 < K and _cand(lo[t], hi[t], b + 1) > c:
+                nhi = _cand(lo[t], hi[t], b + 1) - 1
+            lo[t], hi[t] = c, nhi
+    assert lo == hi
+    fin = np.array([[np.searchsorted(keys, np.uint64(lo[t]), side=s) for s in ("left", "right")]
+                    for t in range(Q)], dtype=np.int64).reshape(Q, 2)
+    g = allgather(torch.from_numpy(fin))  # k_split_final -> all-gather
+    below = np.zeros((world, world - 1), np.int64)
+    upto = np.zeros_like(below)
+    below[:, :Q], upto[:, :Q] = g[:, :, 0], g[:, :, 1]
+    plan = lsbsort.plan_merge(n, world, rank, below, upto)
+    runs, reqs = [None] * world, []
+    for q in range(world):
+        sc, so = int(plan["send_counts"][q]), int(plan["send_displs"][q])
+        rc = int(plan["recv_counts"][q])
+        if q == rank:
+            runs[q] = A[so:so + sc]
+            continue
+        if sc:
+            reqs.append(dist.isend(torch.from_numpy(A[so:so + sc].view(np.uint64).copy()), q))
+        rbuf = torch.empty(2 * rc, dtype=torch.uint64)
+        if rc:
+            reqs.append(dist.irecv(rbuf, q))
+        runs[q] = rbuf
+    for r in reqs:
+        r.wait()
+    runs = [x if isinstance(x, np.ndarray) else x.numpy().view(oracle.ELEM_DTYPE) for x in runs]
+    R = np.concatenate(runs)
+    out = R[np.argsort(R["key"], kind="stable")]  # k_merge2 tree: stable, sources in rank order
+    np.save(os.path.join(result_dir, f"rank{rank}.npy"), out)
+    d.close()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_whole_key_exchange_reproduces_reference(tmp_path, digests, oracle_mod, world):
+    import torch.multiprocessing as mp
+    row = next((r for r in digests["rows"] if r["P"] == world), None)
+    n = row["n"] if row else 100_003
+    mp.start_processes(_merge_worker, args=(world, _free_port(), n, str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    out = np.concatenate([np.load(tmp_path / f"rank{r}.npy") for r in range(world)])
+    if row:
+        assert oracle_mod.digest(out) == row["output"]
+    else:
+        assert np.array_equal(out, oracle_mod.mpi_sort(n, world))

@@ -72,7 +72,8 @@ def _run(tmp_path, world, case):
     return out, meta
 
 
-@pytest.mark.parametrize("world,bits,slices", [(2, 8, 4), (2, 16, 3), (4, 16, 1), (4, 8, 7)])
+@pytest.mark.parametrize("world,bits,slices", [(2, 8, 4), (2, 16, 3), (4, 16, 1), (4, 8, 7),
+                                               (2, 64, 1), (4, 64, 1)])
 def test_processes_reproduce_reference_digest(tmp_path, digests, oracle_mod, world, bits, slices):
     row = next(r for r in digests["rows"] if r["P"] == world)
     case = dict(n=row["n"], bits=bits, slices=slices, mask=None)
@@ -96,6 +97,7 @@ def test_processes_peer_store_exchange(tmp_path, digests, oracle_mod, world, bit
 @pytest.mark.parametrize("world,bits,mask,passes,exchanges", [
     (2, 8, 0x00000000FFFFFFFF, 4, 4),
     (3, 16, 0x00FF0000000000FF, 3, 2),   # digit 0; digit 3's low byte; digits 1, 2 skipped
+    (3, 64, 0x00FF0000000000FF, 2, 1),   # whole-key exchange: local passes on bytes 0 and 6
 ])
 def test_processes_skip_constant_digits(tmp_path, oracle_mod, world, bits, mask, passes, exchanges):
     n = 300_007

@@ -443,7 +443,8 @@ def test_beyond_32bit_indices(lsb_built):
 
 
 # ------------------------------------------------------------- the harness
-@pytest.mark.parametrize("extra", [[], ["--exchange", "peer"], ["--slices", "3", "--radix-bits", "16"]])
+@pytest.mark.parametrize("extra", [[], ["--exchange", "peer"], ["--slices", "3", "--radix-bits", "16"],
+                                   ["--radix-bits", "64"]])
 def test_harness_matches_reference_lines(lsb_built, ref_vectors, extra):
     case = next(c for c in ref_vectors["cases"] if c["n"] == 1000003 and c["P"] == 4)
     exe = lsb_built.HARNESS_PATH
