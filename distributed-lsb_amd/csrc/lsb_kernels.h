@@ -137,6 +137,7 @@ hipError_t launch_plan(const uint64_t* hist, int P, int nb, int me, int64_t n, i
 // rank's {#keys < k*, #keys <= k*} per target.  A is sorted by key.
 constexpr int kSplitCands = 256;
 constexpr int kSplitRounds = 8;
+constexpr int kMergeMaxCuts = 512;  // P * slices cap of the whole-key exchange
 hipError_t launch_split_init(uint64_t* state, int Q, hipStream_t s);
 hipError_t launch_split_cands(const Elem* A, int64_t m, const uint64_t* state, int Q, uint64_t* cnt,
                               hipStream_t s);
@@ -144,13 +145,26 @@ hipError_t launch_split_update(const uint64_t* gathered, int P, int Q, const int
                                uint64_t* state, hipStream_t s);
 hipError_t launch_split_final(const Elem* A, int64_t m, const uint64_t* state, int Q, uint64_t* out,
                               hipStream_t s);
-// Stable merge of two key-sorted runs (a before b on equal keys) into out
-// (na + nb records, disjoint from a and b).  path: merge_path_entries(na + nb)
-// int64 scratch; grid: persistent workgroups (4 per CU).
+// One level of a merge tree: npairs stable merges of two key-sorted runs (a
+// before b on equal keys; nb = 0 copies a) into out (na + nb records,
+// disjoint from a and b).  tile0[p] = first tile of pair p in the level's
+// tile numbering (tiles of kMergeTile outputs), tiles = their total.
+// path: tiles + npairs int64 scratch; grid: persistent workgroups (4 per CU).
 constexpr int kMergeTile = 2048;
-inline int64_t merge_path_entries(int64_t n) { return (n + kMergeTile - 1) / kMergeTile + 1; }
-hipError_t launch_merge2(const Elem* a, int64_t na, const Elem* b, int64_t nb, Elem* out,
-                         int64_t* path, int grid, hipStream_t s);
+constexpr int kMergeMaxPairs = 32;
+struct MergePair {
+  const Elem* a;
+  const Elem* b;
+  Elem* out;
+  int64_t na, nb, tile0;
+};
+struct MergeLevel {
+  MergePair p[kMergeMaxPairs];
+  int npairs;
+  int64_t tiles;
+};
+inline int64_t merge_tiles(int64_t n) { return (n + kMergeTile - 1) / kMergeTile; }
+hipError_t launch_merge_level(const MergeLevel& level, int64_t* path, int grid, hipStream_t s);
 
 // O(n) bit-exact stable-sort check of a rank's here-part (see lsb_verify).
 // first_bad must hold UINT64_MAX before the launch; receives min bad global index.

@@ -18,9 +18,10 @@
 //   k_merge_path / k_merge2
 //       the receiver's placement (:568-575): P sorted runs (one per source, in
 //       rank order) -> one sorted block, by a tree of stable two-way merges
-//       (ties: the left run, i.e. the lower source ranks, first).  Each merge
-//       is merge-path partitioned into 2048-output tiles staged in LDS and
-//       written back as whole, coalesced lines.
+//       (ties: the left run, i.e. the lower source ranks, first).  One launch
+//       pair per tree level merges all of the level's pairs; each merge is
+//       merge-path partitioned into 2048-output tiles staged in LDS and written
+//       back as whole, coalesced lines.
 #include "lsb_kernels.h"
 
 namespace lsb {
@@ -126,15 +127,27 @@ __device__ __forceinline__ int64_t merge_path_global(const Elem* __restrict__ a,
   return lo;
 }
 
-// path[t] = co-rank (records of a) of output position min(t * kMergeTile, na + nb).
-__global__ __launch_bounds__(256) void k_merge_path(const Elem* __restrict__ a, int64_t na,
-                                                    const Elem* __restrict__ b, int64_t nb,
-                                                    int64_t tiles, int64_t* __restrict__ path) {
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (t > tiles) return;
-  const int64_t n = na + nb;
+// Pair p of a merge level covers global tiles [tile0[p], tile0[p + 1]); its
+// path entries are path[tile0[p] + p .. tile0[p + 1] + p] (one more than its
+// tiles).  Pairs are found by a scan of at most kMergeMaxPairs descriptors.
+__device__ __forceinline__ int level_pair(const MergeLevel& L, int64_t tile) {
+  int p = 0;
+  while (p + 1 < L.npairs && L.p[p + 1].tile0 <= tile) ++p;
+  return p;
+}
+
+// Every path entry of the level: co-rank (records of a) of output position
+// min(t * kMergeTile, na + nb) of its pair's tile t.
+__global__ __launch_bounds__(256) void k_merge_path(MergeLevel L, int64_t* __restrict__ path) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= L.tiles + L.npairs) return;
+  int p = 0;  // pair of entry e: entries of pair p start at tile0[p] + p
+  while (p + 1 < L.npairs && L.p[p + 1].tile0 + p + 1 <= e) ++p;
+  const MergePair& q = L.p[p];
+  const int64_t t = e - q.tile0 - p;
+  const int64_t n = q.na + q.nb;
   const int64_t d = t * kMergeTile < n ? t * kMergeTile : n;
-  path[t] = merge_path_global(a, na, b, nb, d);
+  path[e] = merge_path_global(q.a, q.na, q.b, q.nb, d);
 }
 
 constexpr int kMergeBlock = 256;
@@ -149,8 +162,9 @@ __device__ __forceinline__ int merge_slot(int x) {
   return x + (x >> 3);
 }
 
-// Persistent: workgroup w merges tiles w, w + grid, ... (4 per CU, 40 KiB of
-// LDS each).  Per tile of kMergeTile outputs:
+// Persistent: workgroup w merges tiles w, w + grid, ... of the whole level
+// (every pair; 4 workgroups per CU, 40 KiB of LDS each).  Per tile of
+// kMergeTile outputs:
 //   1. its a- and b-ranges (from the tile path) -> LDS, 16-byte loads from
 //      consecutive lanes (a-range first, then the b-range);
 //   2. each thread owns kMergeIpt consecutive outputs: merge path inside the
@@ -159,21 +173,25 @@ __device__ __forceinline__ int merge_slot(int x) {
 //      consecutive lanes, whole 128-byte lines.
 // tools/kbench/merge.hip: this shape runs at the speed of a plain copy of the
 // same bytes; one-shot 4096-record tiles (2 per CU) reach 2/3 of it, threads
-// storing their own outputs (lane-strided lines) 40 %.
-__global__ __launch_bounds__(kMergeBlock) void k_merge2(const Elem* __restrict__ a, int64_t na,
-                                                        const Elem* __restrict__ b, int64_t nb,
-                                                        const int64_t* __restrict__ path,
-                                                        int64_t tiles, Elem* __restrict__ out) {
+// storing their own outputs (lane-strided lines) 40 %.  A pair with nb = 0
+// is a copy through the same path.
+__global__ __launch_bounds__(kMergeBlock) void k_merge2(MergeLevel L, const int64_t* __restrict__ path) {
   __shared__ ulonglong2 tile[kMergeTile + kMergeTile / 8];   // 36 KiB
   __shared__ uint16_t idx[kMergeTile];                       // 4 KiB
-  const int64_t n = na + nb;
   const int t = threadIdx.x;
-  for (int64_t tt = blockIdx.x; tt < tiles; tt += gridDim.x) {
-    const int64_t d0 = tt * kMergeTile;
+  for (int64_t gt = blockIdx.x; gt < L.tiles; gt += gridDim.x) {
+    const int p = level_pair(L, gt);
+    const Elem* __restrict__ a = L.p[p].a;
+    const Elem* __restrict__ b = L.p[p].b;
+    Elem* __restrict__ out = L.p[p].out;
+    const int64_t n = L.p[p].na + L.p[p].nb;
+    const int64_t lt = gt - L.p[p].tile0;
+    const int64_t* pp = path + L.p[p].tile0 + p + lt;
+    const int64_t d0 = lt * kMergeTile;
     const int64_t d1 = d0 + kMergeTile < n ? d0 + kMergeTile : n;
-    const int64_t i0 = path[tt];
+    const int64_t i0 = pp[0];
     const int64_t j0 = d0 - i0;
-    const int ta = (int)(path[tt + 1] - i0);  // records of a in this tile
+    const int ta = (int)(pp[1] - i0);        // records of a in this tile
     const int nt = (int)(d1 - d0);            // ta + tb
     const int tb = nt - ta;
 
@@ -184,8 +202,8 @@ __global__ __launch_bounds__(kMergeBlock) void k_merge2(const Elem* __restrict__
       for (int k = 0; k < kMergeIpt; ++k) {
         const int x = t + k * kMergeBlock;
         if (x < nt) {
-          const Elem* p = x < ta ? a + (i0 + x) : b + (j0 + (x - ta));
-          v[k] = *reinterpret_cast<const ulonglong2*>(p);
+          const Elem* q = x < ta ? a + (i0 + x) : b + (j0 + (x - ta));
+          v[k] = *reinterpret_cast<const ulonglong2*>(q);
         }
       }
 #pragma unroll
@@ -262,18 +280,16 @@ hipError_t launch_split_final(const Elem* A, int64_t m, const uint64_t* state, i
   return hipGetLastError();
 }
 
-hipError_t launch_merge2(const Elem* a, int64_t na, const Elem* b, int64_t nb, Elem* out,
-                         int64_t* path, int grid, hipStream_t s) {
-  const int64_t n = na + nb;
-  if (n == 0) return hipSuccess;
-  const int64_t tiles = (n + kMergeTile - 1) / kMergeTile;
-  hipLaunchKernelGGL(k_merge_path, dim3((unsigned)((tiles + 1 + 255) / 256)), dim3(256), 0, s, a,
-                     na, b, nb, tiles, path);
+hipError_t launch_merge_level(const MergeLevel& level, int64_t* path, int grid, hipStream_t s) {
+  if (level.npairs <= 0 || level.npairs > kMergeMaxPairs) return hipErrorInvalidValue;
+  if (level.tiles == 0) return hipSuccess;
+  const int64_t entries = level.tiles + level.npairs;
+  hipLaunchKernelGGL(k_merge_path, dim3((unsigned)((entries + 255) / 256)), dim3(256), 0, s, level,
+                     path);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  const int64_t g = tiles < grid ? tiles : grid;
-  hipLaunchKernelGGL(k_merge2, dim3((unsigned)g), dim3(kMergeBlock), 0, s, a, na, b, nb, path, tiles,
-                     out);
+  const int64_t g = level.tiles < grid ? level.tiles : grid;
+  hipLaunchKernelGGL(k_merge2, dim3((unsigned)g), dim3(kMergeBlock), 0, s, level, path);
   return hipGetLastError();
 }
 

@@ -103,6 +103,8 @@ struct Rank {
   uint64_t* split_fin_gather = nullptr; // [P][Q][2]
   uint64_t* split_h = nullptr;          // pinned mirror of split_fin_gather
   int64_t* merge_path = nullptr;        // merge-path tile boundaries
+  int split_q = 0, split_S = 0;         // geometry the split buffers were sized for
+  std::vector<int64_t> mcut;            // [P][P * S + 1] cuts of every source (host)
   std::vector<int64_t> send_counts, send_displs, recv_counts, recv_displs;
 };
 
@@ -904,34 +906,50 @@ int sort_onesweep(lsb_ctx* c) {
 // placement of :568-575).  Same output as 64 / 8 or 64 / 16 exchanges: the
 // stable order by key, ties by input position.
 
-// Targets of the splitter search: global positions T_q = q * per for
-// q = 1 .. Q, the q with q * per < n (beyond n a source sends everything
-// below, so its cut is its whole block).
-int merge_targets(const lsb_ctx* c) {
-  int Q = 0;
-  while (Q + 1 < c->P && (int64_t)(Q + 1) * c->per < c->n) ++Q;
-  return Q;
+// Cut positions of the exchange: owner q's block [q * per, q * per + here_q)
+// is cut into S slices (sub-blocks) at q * per + part(here_q, j, S); cut k =
+// q * S + j, plus k = P * S at n.  Every cut strictly inside (0, n) is a
+// target of the splitter search.  S = 1 gives the owner boundaries q * per.
+// Slices let the owner merge slice j while slice j + 1 is on the wire.
+struct MergeGeom {
+  int S = 1;
+  std::vector<int64_t> pos;   // [P * S + 1] global cut positions, nondecreasing
+  std::vector<int> target;    // cut indices k with 0 < pos[k] < n (splitter targets)
+};
+
+MergeGeom merge_geometry(int64_t n, int P, int slices) {
+  MergeGeom g;
+  const int64_t per = div_ceil(n, P);
+  g.S = std::max(1, std::min(slices, lsb::kMergeMaxCuts / P));
+  g.pos.resize((size_t)P * g.S + 1);
+  for (int q = 0; q < P; ++q) {
+    const int64_t h = here_of(n, P, q);
+    for (int j = 0; j < g.S; ++j)
+      g.pos[(size_t)q * g.S + j] = std::min(n, (int64_t)q * per + part(h, j, g.S));
+  }
+  g.pos[(size_t)P * g.S] = n;
+  for (size_t k = 0; k < g.pos.size(); ++k)
+    if (g.pos[k] > 0 && g.pos[k] < n) g.target.push_back((int)k);
+  return g;
 }
 
-// Host side of the plan: from every rank's {#keys < k*_q, #keys <= k*_q}
-// (fin[(s * Q + q - 1) * 2 + {0,1}]) the cut of source s at T_q is
-//   below_s + min(equal_s, max(0, T_q - sum_s below_s - sum_{s' < s} equal_s'))
-// (equal keys in rank order = input order), and
-//   send to q:  my cuts [q, q + 1);  receive from s: s's cuts [me, me + 1).
-int plan_merge_core(int64_t n, int P, int me, int Q, const uint64_t* fin, int64_t* sc, int64_t* sd,
-                    int64_t* rc, int64_t* rd) {
-  const int64_t per = div_ceil(n, P);
-  // cut[s * (P + 1) + q], q = 0 .. P
-  std::vector<int64_t> cut((size_t)P * (P + 1));
-  for (int s = 0; s < P; ++s) {
-    cut[(size_t)s * (P + 1)] = 0;
-    for (int q = 1; q <= P; ++q) cut[(size_t)s * (P + 1) + q] = here_of(n, P, s);
-  }
-  for (int q = 1; q <= Q; ++q) {
-    const int64_t T = (int64_t)q * per;
+// Host side of the plan: from every rank's {#keys < k*_t, #keys <= k*_t}
+// (fin[(s * Q + t) * 2 + {0,1}], t over g.target) the cut of source s at
+// position T is
+//   below_s + min(equal_s, max(0, T - sum_s below_s - sum_{s' < s} equal_s'))
+// (equal keys in rank order = input order).  cut[s * (K + 1) + k].
+int merge_cuts(int64_t n, int P, const MergeGeom& g, const uint64_t* fin, std::vector<int64_t>& cut) {
+  const size_t K1 = g.pos.size();
+  const int Q = (int)g.target.size();
+  cut.assign((size_t)P * K1, 0);
+  for (int s = 0; s < P; ++s)
+    for (size_t k = 0; k < K1; ++k) cut[s * K1 + k] = g.pos[k] >= n ? here_of(n, P, s) : 0;
+  for (int t = 0; t < Q; ++t) {
+    const int k = g.target[t];
+    const int64_t T = g.pos[k];
     int64_t below = 0, all = 0;
     for (int s = 0; s < P; ++s) {
-      const uint64_t b = fin[((size_t)s * Q + q - 1) * 2], u = fin[((size_t)s * Q + q - 1) * 2 + 1];
+      const uint64_t b = fin[((size_t)s * Q + t) * 2], u = fin[((size_t)s * Q + t) * 2 + 1];
       if (b > u || (int64_t)u > here_of(n, P, s))
         return fail(LSB_ERR_INVALID, "plan_merge", "counts out of range");
       below += (int64_t)b;
@@ -940,18 +958,29 @@ int plan_merge_core(int64_t n, int P, int me, int Q, const uint64_t* fin, int64_
     if (!(below <= T && T < all)) return fail(LSB_ERR_INVALID, "plan_merge", "target not bracketed");
     int64_t rem = T - below;
     for (int s = 0; s < P; ++s) {
-      const int64_t b = (int64_t)fin[((size_t)s * Q + q - 1) * 2];
-      const int64_t eq = (int64_t)fin[((size_t)s * Q + q - 1) * 2 + 1] - b;
-      const int64_t take = std::min(eq, rem);
-      cut[(size_t)s * (P + 1) + q] = b + take;
+      const int64_t b = (int64_t)fin[((size_t)s * Q + t) * 2];
+      const int64_t take = std::min((int64_t)fin[((size_t)s * Q + t) * 2 + 1] - b, rem);
+      cut[s * K1 + k] = b + take;
       rem -= take;
     }
   }
+  for (int s = 0; s < P; ++s)
+    for (size_t k = 0; k + 1 < K1; ++k)
+      if (cut[s * K1 + k + 1] < cut[s * K1 + k])
+        return fail(LSB_ERR_INVALID, "plan_merge", "cuts not monotone");
+  return LSB_OK;
+}
+
+// Owner-level counts of rank `me` (lsb_plan_merge): send [cut_q, cut_{q+1}) to
+// q, receive [cut_me, cut_{me+1}) of every s.
+int merge_owner_counts(int64_t n, int P, int me, const MergeGeom& g, const std::vector<int64_t>& cut,
+                       int64_t* sc, int64_t* sd, int64_t* rc, int64_t* rd) {
+  const size_t K1 = g.pos.size();
+  const int S = g.S;
   int64_t a = 0, b = 0;
   for (int q = 0; q < P; ++q) {
-    sc[q] = cut[(size_t)me * (P + 1) + q + 1] - cut[(size_t)me * (P + 1) + q];
-    rc[q] = cut[(size_t)q * (P + 1) + me + 1] - cut[(size_t)q * (P + 1) + me];
-    if (sc[q] < 0 || rc[q] < 0) return fail(LSB_ERR_INVALID, "plan_merge", "cuts not monotone");
+    sc[q] = cut[(size_t)me * K1 + (size_t)(q + 1) * S] - cut[(size_t)me * K1 + (size_t)q * S];
+    rc[q] = cut[(size_t)q * K1 + (size_t)(me + 1) * S] - cut[(size_t)q * K1 + (size_t)me * S];
     sd[q] = a;
     rd[q] = b;
     a += sc[q];
@@ -961,11 +990,17 @@ int plan_merge_core(int64_t n, int P, int me, int Q, const uint64_t* fin, int64_
   return LSB_OK;
 }
 
-int merge_ensure(lsb_ctx* c, Rank& r, int Q) {
+int merge_ensure(lsb_ctx* c, Rank& r, const MergeGeom& g) {
   HIP_TRY(hipSetDevice(r.dev));
   if (!r.R) LSB_TRY(dev_alloc(&r.R, (size_t)c->per));
-  if (!r.merge_path) LSB_TRY(dev_alloc(&r.merge_path, (size_t)lsb::merge_path_entries(c->per)));
-  if (r.split_state || Q == 0) return LSB_OK;
+  if (!r.merge_path)
+    LSB_TRY(dev_alloc(&r.merge_path, (size_t)(lsb::merge_tiles(c->per) + 2 * lsb::kMergeMaxPairs + 1)));
+  const int Q = (int)g.target.size();
+  if (Q == 0 || (r.split_state && r.split_q == Q && r.split_S == g.S)) return LSB_OK;
+  for (void* p : {(void*)r.split_state, (void*)r.split_targets, (void*)r.split_cnt,
+                  (void*)r.split_gather, (void*)r.split_fin, (void*)r.split_fin_gather})
+    (void)hipFree(p);
+  (void)hipHostFree(r.split_h);
   const size_t P = (size_t)c->P, K = lsb::kSplitCands;
   LSB_TRY(dev_alloc(&r.split_state, 2 * (size_t)Q));
   LSB_TRY(dev_alloc(&r.split_targets, (size_t)Q));
@@ -975,8 +1010,10 @@ int merge_ensure(lsb_ctx* c, Rank& r, int Q) {
   LSB_TRY(dev_alloc(&r.split_fin_gather, P * 2 * Q));
   LSB_TRY(host_alloc(&r.split_h, P * 2 * Q));
   std::vector<int64_t> t(Q);
-  for (int q = 1; q <= Q; ++q) t[q - 1] = (int64_t)q * c->per;
+  for (int i = 0; i < Q; ++i) t[i] = g.pos[g.target[i]];
   HIP_TRY(hipMemcpy(r.split_targets, t.data(), sizeof(int64_t) * Q, hipMemcpyHostToDevice));
+  r.split_q = Q;
+  r.split_S = g.S;
   return LSB_OK;
 }
 
@@ -1027,52 +1064,106 @@ int sort_local_rank(lsb_ctx* c, Rank& r, int* passes, uint64_t* varying) {
   return LSB_OK;
 }
 
-// The owner's P sorted runs (source order) -> one sorted block in A: a tree
-// of stable two-way merges, adjacent runs paired so the lower ranks stay on
-// the left.  Level k writes B (k even) or A (k odd); a run without a partner
-// is copied.  Ends with the block in A (swapped in if it landed in B).
-int merge_runs(lsb_ctx* c, Rank& r) {
+// Records of source s in owner r's slice j, where they sit in R, and the
+// slice's output range [lo, hi) of r's block.
+struct SliceRun {
+  int64_t len, roff;
+};
+
+void slice_runs(const lsb_ctx* c, const Rank& r, const MergeGeom& g, int j, std::vector<SliceRun>& out,
+                int64_t* lo, int64_t* hi) {
+  const size_t K1 = g.pos.size();
+  const int64_t base = (int64_t)r.rank * c->per;
+  const size_t k = (size_t)r.rank * g.S + j;
+  *lo = g.pos[k] - base;
+  *hi = g.pos[k + 1] - base;
+  if (*lo < 0) *lo = 0;
+  if (*hi < *lo) *hi = *lo;
+  out.resize(c->P);
+  int64_t off = *lo;
+  for (int s = 0; s < c->P; ++s) {
+    out[s].len = r.mcut[s * K1 + k + 1] - r.mcut[s * K1 + k];
+    out[s].roff = off;
+    off += out[s].len;
+  }
+}
+
+// Levels of the merge tree over `runs` runs (a single run is one copy level).
+int merge_levels(size_t runs) {
+  int L = 0;
+  for (size_t m = runs; m > 1; m = (m + 1) / 2) ++L;
+  return L > 0 ? L : 1;
+}
+
+// Merge slice j of owner r on r.pstream: its P runs (source order; my own
+// straight out of A) -> F[lo, hi), F = B or R.  A tree of stable two-way
+// merges, one launch per level, adjacent runs paired so the lower ranks stay
+// on the left; level l writes B (l even) or R (l odd): the slice's own region
+// of R is free once level 0 has read it, and A, still being sent from, is
+// never written.  A result that ends in the other buffer is copied to F
+// (only slices with fewer non-empty runs than the rest).
+int merge_slice(lsb_ctx* c, Rank& r, const MergeGeom& g, int j, Elem* F) {
   struct Run {
     const Elem* p;
     int64_t n;
   };
+  std::vector<SliceRun> sr;
+  int64_t lo = 0, hi = 0;
+  slice_runs(c, r, g, j, sr, &lo, &hi);
+  if (hi == lo) return LSB_OK;
+  const size_t K1 = g.pos.size();
   std::vector<Run> runs;
   for (int s = 0; s < c->P; ++s) {
-    if (r.recv_counts[s] == 0) continue;
-    runs.push_back({s == r.rank ? r.A + r.send_displs[s] : r.R + r.recv_displs[s], r.recv_counts[s]});
+    if (sr[s].len == 0) continue;
+    const Elem* p = s == r.rank ? r.A + r.mcut[s * K1 + (size_t)r.rank * g.S + j] : r.R + sr[s].roff;
+    runs.push_back({p, sr[s].len});
   }
-  if (runs.empty() || (runs.size() == 1 && runs[0].p == r.A)) return LSB_OK;
-  HIP_TRY(hipSetDevice(r.dev));
-  Timer t(c, &r, LSB_K_PLACE);
-  int level = 0;
-  while (runs.size() > 1 || level == 0) {
-    Elem* dst = (level % 2 == 0) ? r.B : r.A;
+  Timer t(c, &r, LSB_K_PLACE, r.pstream);
+  const int grid = 2 * max_chunks_for_device(r.dev);
+  const int L = merge_levels(runs.size());
+  for (int level = 0; level < L; ++level) {
+    Elem* dst = (level % 2 == 0 ? r.B : r.R) + lo;
+    lsb::MergeLevel lv{};
     std::vector<Run> next;
     int64_t off = 0;
     for (size_t i = 0; i < runs.size(); i += 2) {
-      if (i + 1 < runs.size()) {
-        HIP_TRY(lsb::launch_merge2(runs[i].p, runs[i].n, runs[i + 1].p, runs[i + 1].n, dst + off,
-                                   r.merge_path, 2 * max_chunks_for_device(r.dev), r.stream));
-        next.push_back({dst + off, runs[i].n + runs[i + 1].n});
-      } else {
-        HIP_TRY(hipMemcpyAsync(dst + off, runs[i].p, (size_t)runs[i].n * sizeof(Elem),
-                               hipMemcpyDeviceToDevice, r.stream));
-        next.push_back({dst + off, runs[i].n});
-      }
-      off += next.back().n;
+      const bool pair = i + 1 < runs.size();
+      lsb::MergePair& m = lv.p[lv.npairs++];
+      m.a = runs[i].p;
+      m.na = runs[i].n;
+      m.b = pair ? runs[i + 1].p : runs[i].p;
+      m.nb = pair ? runs[i + 1].n : 0;
+      m.out = dst + off;
+      m.tile0 = lv.tiles;
+      lv.tiles += lsb::merge_tiles(m.na + m.nb);
+      next.push_back({dst + off, m.na + m.nb});
+      off += m.na + m.nb;
     }
+    HIP_TRY(lsb::launch_merge_level(lv, r.merge_path, grid, r.pstream));
     runs.swap(next);
-    ++level;
   }
-  if (level % 2 == 1) std::swap(r.A, r.B);  // the last level wrote B
+  Elem* fin = (L - 1) % 2 == 0 ? r.B : r.R;
+  if (fin != F)
+    HIP_TRY(hipMemcpyAsync(F + lo, fin + lo, (size_t)(hi - lo) * sizeof(Elem), hipMemcpyDeviceToDevice,
+                           r.pstream));
   return LSB_OK;
+}
+
+// Slice j of the all-to-all has arrived on r.stream: merge it on r.pstream
+// while the next slice is on the wire.
+int merge_slice_async(lsb_ctx* c, Rank& r, const MergeGeom& g, int j, Elem* F) {
+  HIP_TRY(hipSetDevice(r.dev));
+  HIP_TRY(hipEventRecord(r.pevent, r.stream));
+  HIP_TRY(hipStreamWaitEvent(r.pstream, r.pevent, 0));
+  return merge_slice(c, r, g, j, F);
 }
 
 int exchange_merge(lsb_ctx* c) {
   const int P = c->P;
-  const int Q = merge_targets(c);
-  const size_t K = lsb::kSplitCands;
-  for (Rank& r : c->ranks) LSB_TRY(merge_ensure(c, r, Q));
+  const MergeGeom g = merge_geometry(c->n, P, c->slices);
+  const int Q = (int)g.target.size();
+  const size_t K = lsb::kSplitCands, K1 = g.pos.size();
+  for (Rank& r : c->ranks) LSB_TRY(merge_ensure(c, r, g));
   // 1. splitter search: kSplitRounds rounds of candidate counts, all-gathered.
   if (Q > 0) {
     for (Rank& r : c->ranks) {
@@ -1105,48 +1196,62 @@ int exchange_merge(lsb_ctx* c) {
                              hipMemcpyDeviceToHost, r.stream));
     }
   }
-  // 2. the plan, on the host (the all-to-all takes host counts)
+  // 2. the cuts, on the host (the all-to-all takes host counts)
   for (Rank& r : c->ranks) {
     HIP_TRY(hipSetDevice(r.dev));
     HIP_TRY(hipStreamSynchronize(r.stream));
-    LSB_TRY(plan_merge_core(c->n, P, r.rank, Q, r.split_h, r.send_counts.data(),
-                            r.send_displs.data(), r.recv_counts.data(), r.recv_displs.data()));
+    LSB_TRY(merge_cuts(c->n, P, g, r.split_h, r.mcut));
   }
-  // 3. one all-to-all-v of contiguous ranges (the self range stays in A)
-  if (c->mode == Mode::kLoopback) {
-    for (Rank& q : c->ranks) {
-      HIP_TRY(hipSetDevice(q.dev));
-      Timer t(c, &q, LSB_K_EXCHANGE);
-      for (Rank& s : c->ranks) {
-        if (s.rank == q.rank || s.send_counts[q.rank] == 0) continue;
-        if (s.send_counts[q.rank] != q.recv_counts[s.rank])
-          return fail(LSB_ERR_STATE, "exchange_merge", "send/recv count mismatch");
-        HIP_TRY(hipMemcpyAsync(q.R + q.recv_displs[s.rank], s.A + s.send_displs[q.rank],
-                               (size_t)q.recv_counts[s.rank] * sizeof(Elem), hipMemcpyDefault,
-                               q.stream));
+  // 3. slice by slice: all-to-all-v of contiguous ranges (my own range stays
+  //    in A), then the slice's merge on the placement stream.  The merged
+  //    block lands in B or R, whichever the last level of a P-run tree writes.
+  const bool final_b = (merge_levels((size_t)P) - 1) % 2 == 0;
+  std::vector<SliceRun> sr;
+  int64_t lo = 0, hi = 0;
+  for (int j = 0; j < g.S; ++j) {
+    if (c->mode == Mode::kLoopback) {
+      for (Rank& q : c->ranks) {
+        HIP_TRY(hipSetDevice(q.dev));
+        Timer t(c, &q, LSB_K_EXCHANGE);
+        slice_runs(c, q, g, j, sr, &lo, &hi);
+        for (Rank& s : c->ranks) {
+          if (s.rank == q.rank || sr[s.rank].len == 0) continue;
+          HIP_TRY(hipMemcpyAsync(q.R + sr[s.rank].roff, s.A + q.mcut[s.rank * K1 + (size_t)q.rank * g.S + j],
+                                 (size_t)sr[s.rank].len * sizeof(Elem), hipMemcpyDefault, q.stream));
+        }
       }
+      for (Rank& q : c->ranks) LSB_TRY(merge_slice_async(c, q, g, j, final_b ? q.B : q.R));
+    } else {
+      Rank& r = c->ranks[0];
+      HIP_TRY(hipSetDevice(r.dev));
+      slice_runs(c, r, g, j, sr, &lo, &hi);
+      std::vector<size_t> sc(P), sd(P), rc(P), rdp(P);
+      for (int q = 0; q < P; ++q) {
+        const size_t kq = (size_t)q * g.S + j;
+        sc[q] = q == r.rank ? 0 : (size_t)(r.mcut[(size_t)r.rank * K1 + kq + 1] - r.mcut[(size_t)r.rank * K1 + kq]) * 2;
+        sd[q] = (size_t)r.mcut[(size_t)r.rank * K1 + kq] * 2;
+        rc[q] = q == r.rank ? 0 : (size_t)sr[q].len * 2;
+        rdp[q] = (size_t)sr[q].roff * 2;
+      }
+      {
+        Timer t(c, &r, LSB_K_EXCHANGE);
+        LSB_TRY(coll_alltoallv_u64(c, r, reinterpret_cast<const uint64_t*>(r.A), sc.data(), sd.data(),
+                                   reinterpret_cast<uint64_t*>(r.R), rc.data(), rdp.data()));
+      }
+      LSB_TRY(merge_slice_async(c, r, g, j, final_b ? r.B : r.R));
     }
-    // No rank's merge may overwrite its A while another rank still copies from it.
+  }
+  // 4. the merged block (B or R) becomes A: every rank's sends out of A are done
+  //    (loopback: all copies; RCCL / ops: my stream finished the collectives).
+  if (c->mode == Mode::kLoopback)
     for (Rank& r : c->ranks) {
       HIP_TRY(hipSetDevice(r.dev));
       HIP_TRY(hipStreamSynchronize(r.stream));
     }
-  } else {
-    Rank& r = c->ranks[0];
-    HIP_TRY(hipSetDevice(r.dev));
-    std::vector<size_t> sc(P), sd(P), rc(P), rdp(P);
-    for (int q = 0; q < P; ++q) {
-      sc[q] = q == r.rank ? 0 : (size_t)r.send_counts[q] * 2;
-      rc[q] = q == r.rank ? 0 : (size_t)r.recv_counts[q] * 2;
-      sd[q] = (size_t)r.send_displs[q] * 2;
-      rdp[q] = (size_t)r.recv_displs[q] * 2;
-    }
-    Timer t(c, &r, LSB_K_EXCHANGE);
-    LSB_TRY(coll_alltoallv_u64(c, r, reinterpret_cast<const uint64_t*>(r.A), sc.data(), sd.data(),
-                               reinterpret_cast<uint64_t*>(r.R), rc.data(), rdp.data()));
+  for (Rank& r : c->ranks) {
+    LSB_TRY(join_place(r));
+    std::swap(r.A, final_b ? r.B : r.R);
   }
-  // 4. merge the runs
-  for (Rank& r : c->ranks) LSB_TRY(merge_runs(c, r));
   return LSB_OK;
 }
 
@@ -1710,21 +1815,20 @@ int lsb_plan_merge(int64_t n_total, int P, int me, const int64_t* below, const i
   if (P < 1 || P > 64 || me < 0 || me >= P || n_total < 0 || (P > 1 && (!below || !upto)) ||
       !send_counts || !send_displs || !recv_counts || !recv_displs)
     return fail(LSB_ERR_INVALID, "lsb_plan_merge", "arguments");
-  lsb_ctx c;
-  c.n = n_total;
-  c.P = P;
-  c.per = div_ceil(n_total, P);
-  const int Q = merge_targets(&c);
+  const MergeGeom g = merge_geometry(n_total, P, 1);  // targets q * per, q = 1 .. P-1 below n
+  const int Q = (int)g.target.size();
   std::vector<uint64_t> fin((size_t)P * 2 * Q);
   for (int s = 0; s < P; ++s)
-    for (int q = 0; q < Q; ++q) {
-      const int64_t b = below[(size_t)s * (P - 1) + q], u = upto[(size_t)s * (P - 1) + q];
+    for (int t = 0; t < Q; ++t) {
+      const int q = g.target[t];  // cut index == owner (S = 1)
+      const int64_t b = below[(size_t)s * (P - 1) + q - 1], u = upto[(size_t)s * (P - 1) + q - 1];
       if (b < 0 || u < 0) return fail(LSB_ERR_INVALID, "lsb_plan_merge", "negative count");
-      fin[((size_t)s * Q + q) * 2] = (uint64_t)b;
-      fin[((size_t)s * Q + q) * 2 + 1] = (uint64_t)u;
+      fin[((size_t)s * Q + t) * 2] = (uint64_t)b;
+      fin[((size_t)s * Q + t) * 2 + 1] = (uint64_t)u;
     }
-  return plan_merge_core(n_total, P, me, Q, fin.data(), send_counts, send_displs, recv_counts,
-                         recv_displs);
+  std::vector<int64_t> cut;
+  LSB_TRY(merge_cuts(n_total, P, g, fin.data(), cut));
+  return merge_owner_counts(n_total, P, me, g, cut, send_counts, send_displs, recv_counts, recv_displs);
 }
 
 int lsb_plan_exchange(int64_t n_total, int P, int me, int nb, const int64_t* hist,
