@@ -149,7 +149,7 @@ hipError_t launch_split_final(const Elem* A, int64_t m, const uint64_t* state, i
 // before b on equal keys; nb = 0 copies a) into out (na + nb records,
 // disjoint from a and b).  tile0[p] = first tile of pair p in the level's
 // tile numbering (tiles of kMergeTile outputs), tiles = their total.
-// path: tiles + npairs int64 scratch; grid: persistent workgroups (4 per CU).
+// path: tiles + npairs int64 scratch; grid: persistent workgroups (3 per CU).
 constexpr int kMergeTile = 2048;
 constexpr int kMergeMaxPairs = 32;
 struct MergePair {

@@ -24,6 +24,13 @@
 //       back as whole, coalesced lines.
 #include "lsb_kernels.h"
 
+#ifdef LSB_DEBUG
+#include <cassert>
+#define LSB_MERGE_ASSERT(c) assert(c)
+#else
+#define LSB_MERGE_ASSERT(c) ((void)0)
+#endif
+
 namespace lsb {
 namespace {
 
@@ -127,12 +134,15 @@ __device__ __forceinline__ int64_t merge_path_global(const Elem* __restrict__ a,
   return lo;
 }
 
-// Pair p of a merge level covers global tiles [tile0[p], tile0[p + 1]); its
-// path entries are path[tile0[p] + p .. tile0[p + 1] + p] (one more than its
-// tiles).  Pairs are found by a scan of at most kMergeMaxPairs descriptors.
-__device__ __forceinline__ int level_pair(const MergeLevel& L, int64_t tile) {
+// Pair of a merge level that holds global tile x (kPathEntries: path entry
+// x, k_merge_path): the last p with first[p] <= x, where pair p's tiles start
+// at tile0[p] and its path entries at tile0[p] + p (one more entry than
+// tiles).  The descriptors stay kernel arguments, indexed in place.
+template <bool kPathEntries>
+__device__ __forceinline__ int level_pair(const MergeLevel& L, int64_t x) {
   int p = 0;
-  while (p + 1 < L.npairs && L.p[p + 1].tile0 <= tile) ++p;
+  for (int q = 1; q < L.npairs; ++q)
+    if ((kPathEntries ? L.p[q].tile0 + q : L.p[q].tile0) <= x) p = q;
   return p;
 }
 
@@ -141,8 +151,7 @@ __device__ __forceinline__ int level_pair(const MergeLevel& L, int64_t tile) {
 __global__ __launch_bounds__(256) void k_merge_path(MergeLevel L, int64_t* __restrict__ path) {
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (e >= L.tiles + L.npairs) return;
-  int p = 0;  // pair of entry e: entries of pair p start at tile0[p] + p
-  while (p + 1 < L.npairs && L.p[p + 1].tile0 + p + 1 <= e) ++p;
+  const int p = level_pair<true>(L, e);
   const MergePair& q = L.p[p];
   const int64_t t = e - q.tile0 - p;
   const int64_t n = q.na + q.nb;
@@ -153,40 +162,36 @@ __global__ __launch_bounds__(256) void k_merge_path(MergeLevel L, int64_t* __res
 constexpr int kMergeBlock = 256;
 constexpr int kMergeIpt = kMergeTile / kMergeBlock;  // 8 outputs per thread
 
-// LDS slot of tile record x: one 16-byte pad slot after every 8 records.  A
-// thread's merge reads records ~4 apart from its neighbour's (8 outputs per
-// thread, half from each run); without the pad that stride puts many lanes
-// on the same banks.  Reads past a run's end are clamped (never used).
-__device__ __forceinline__ int merge_slot(int x) {
-  x = x < kMergeTile - 1 ? x : kMergeTile - 1;
-  return x + (x >> 3);
-}
-
 // Persistent: workgroup w merges tiles w, w + grid, ... of the whole level
-// (every pair; 4 workgroups per CU, 40 KiB of LDS each).  Per tile of
-// kMergeTile outputs:
-//   1. its a- and b-ranges (from the tile path) -> LDS, 16-byte loads from
-//      consecutive lanes (a-range first, then the b-range);
+// (every pair; 3 workgroups per CU, 20 KiB of LDS each, so RCCL's kernel,
+// 37 KiB of LDS, still fits on every CU while a level runs beside an
+// all-to-all).  Per tile of kMergeTile outputs:
+//   1. the KEYS of its a- and b-ranges (from the tile path) -> LDS, from
+//      16-byte loads of consecutive lanes (a-range first, then the b-range);
 //   2. each thread owns kMergeIpt consecutive outputs: merge path inside the
-//      tile, then a sequential merge that writes the LDS slot of every output;
-//   3. output x of the tile = LDS record idx[x]: 16-byte stores from
-//      consecutive lanes, whole 128-byte lines.
-// tools/kbench/merge.hip: this shape runs at the speed of a plain copy of the
-// same bytes; one-shot 4096-record tiles (2 per CU) reach 2/3 of it, threads
-// storing their own outputs (lane-strided lines) 40 %.  A pair with nb = 0
-// is a copy through the same path.
+//      tile, then a sequential merge that writes the source index of every
+//      output;
+//   3. output x of the tile = record idx[x] of the tile's input, loaded
+//      again (its line was fetched by step 1 and is still in L2) and stored
+//      by consecutive lanes: whole 128-byte lines.
+// tools/kbench/merge2.hip: keys-only staging streams at 5.2 TB/s (a plain
+// tile copy through LDS: 5.1), the full 16-byte records staged in LDS at
+// 2.5 TB/s (2 WG/CU) to 3.7 TB/s (4 WG/CU).  A pair with nb = 0 is a copy
+// through the same path.
 __global__ __launch_bounds__(kMergeBlock) void k_merge2(MergeLevel L, const int64_t* __restrict__ path) {
-  __shared__ ulonglong2 tile[kMergeTile + kMergeTile / 8];   // 36 KiB
-  __shared__ uint16_t idx[kMergeTile];                       // 4 KiB
+  __shared__ uint64_t keys[kMergeTile];  // 16 KiB
+  __shared__ uint16_t idx[kMergeTile];   // 4 KiB
   const int t = threadIdx.x;
+  auto key = [&](int x) { return keys[x < kMergeTile - 1 ? x : kMergeTile - 1]; };  // run ends: never used
   for (int64_t gt = blockIdx.x; gt < L.tiles; gt += gridDim.x) {
-    const int p = level_pair(L, gt);
-    const Elem* __restrict__ a = L.p[p].a;
-    const Elem* __restrict__ b = L.p[p].b;
-    Elem* __restrict__ out = L.p[p].out;
-    const int64_t n = L.p[p].na + L.p[p].nb;
-    const int64_t lt = gt - L.p[p].tile0;
-    const int64_t* pp = path + L.p[p].tile0 + p + lt;
+    const int p = level_pair<false>(L, gt);
+    const MergePair& q = L.p[p];
+    const Elem* __restrict__ a = q.a;
+    const Elem* __restrict__ b = q.b;
+    Elem* __restrict__ out = q.out;
+    const int64_t n = q.na + q.nb;
+    const int64_t lt = gt - q.tile0;
+    const int64_t* pp = path + q.tile0 + p + lt;
     const int64_t d0 = lt * kMergeTile;
     const int64_t d1 = d0 + kMergeTile < n ? d0 + kMergeTile : n;
     const int64_t i0 = pp[0];
@@ -195,21 +200,18 @@ __global__ __launch_bounds__(kMergeBlock) void k_merge2(MergeLevel L, const int6
     const int nt = (int)(d1 - d0);            // ta + tb
     const int tb = nt - ta;
 
-    // 1. stage
+    // 1. stage the keys
     {
-      ulonglong2 v[kMergeIpt];
+      uint64_t v[kMergeIpt];
 #pragma unroll
       for (int k = 0; k < kMergeIpt; ++k) {
         const int x = t + k * kMergeBlock;
-        if (x < nt) {
-          const Elem* q = x < ta ? a + (i0 + x) : b + (j0 + (x - ta));
-          v[k] = *reinterpret_cast<const ulonglong2*>(q);
-        }
+        if (x < nt) v[k] = (x < ta ? a + (i0 + x) : b + (j0 + (x - ta)))->key;
       }
 #pragma unroll
       for (int k = 0; k < kMergeIpt; ++k) {
         const int x = t + k * kMergeBlock;
-        if (x < nt) tile[merge_slot(x)] = v[k];
+        if (x < nt) keys[x] = v[k];
       }
     }
     __syncthreads();
@@ -220,29 +222,34 @@ __global__ __launch_bounds__(kMergeBlock) void k_merge2(MergeLevel L, const int6
       int lo = dl > tb ? dl - tb : 0, hi = dl < ta ? dl : ta;
       while (lo < hi) {
         const int mid = (lo + hi) >> 1;
-        if (tile[merge_slot(mid)].x <= tile[merge_slot(ta + dl - 1 - mid)].x) lo = mid + 1;
+        if (key(mid) <= key(ta + dl - 1 - mid)) lo = mid + 1;
         else hi = mid;
       }
       int ia = lo, ib = dl - lo;
-      uint64_t ka = tile[merge_slot(ia)].x, kb = tile[merge_slot(ta + ib)].x;
+      uint64_t ka = key(ia), kb = key(ta + ib);
       const int end = dl + kMergeIpt < nt ? dl + kMergeIpt : nt;
       for (int k = dl; k < end; ++k) {
         const bool take_a = ib >= tb || (ia < ta && ka <= kb);
-        idx[k] = (uint16_t)merge_slot(take_a ? ia : ta + ib);
+        idx[k] = (uint16_t)(take_a ? ia : ta + ib);
         if (take_a) ++ia;
         else ++ib;
-        const uint64_t nk = tile[merge_slot(take_a ? ia : ta + ib)].x;
+        const uint64_t nk = key(take_a ? ia : ta + ib);
         if (take_a) ka = nk;
         else kb = nk;
       }
     }
     __syncthreads();
 
-    // 3. write out in output order
+    // 3. gather the records in output order and write them out
 #pragma unroll
     for (int k = 0; k < kMergeIpt; ++k) {
       const int x = t + k * kMergeBlock;
-      if (x < nt) *reinterpret_cast<ulonglong2*>(out + (d0 + x)) = tile[idx[x]];
+      if (x < nt) {
+        const int s = idx[x];
+        const Elem* src = s < ta ? a + (i0 + s) : b + (j0 + (s - ta));
+        LSB_MERGE_ASSERT(d0 + x < n);
+        *reinterpret_cast<ulonglong2*>(out + (d0 + x)) = *reinterpret_cast<const ulonglong2*>(src);
+      }
     }
     __syncthreads();  // the tile's LDS is reused
   }

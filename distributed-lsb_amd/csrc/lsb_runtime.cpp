@@ -1119,7 +1119,9 @@ int merge_slice(lsb_ctx* c, Rank& r, const MergeGeom& g, int j, Elem* F) {
     runs.push_back({p, sr[s].len});
   }
   Timer t(c, &r, LSB_K_PLACE, r.pstream);
-  const int grid = 2 * max_chunks_for_device(r.dev);
+  // 3 merge workgroups per CU (max_chunks = 2 per CU): 60 KiB of LDS, so
+  // RCCL's kernel for the next slice (37 KiB) still finds room on every CU.
+  const int grid = 3 * max_chunks_for_device(r.dev) / 2;
   const int L = merge_levels(runs.size());
   for (int level = 0; level < L; ++level) {
     Elem* dst = (level % 2 == 0 ? r.B : r.R) + lo;
