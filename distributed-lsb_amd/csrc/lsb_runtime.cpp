@@ -124,7 +124,7 @@ struct lsb_ctx {
   bool timing = false;
   bool force_exchange = false;
   bool skip_constant = true;  // lsb_sort skips digits on which all keys agree
-  int slices = 4;             // exchange slices (placement overlaps the next slice)
+  int slices = 0;             // exchange slices (placement overlaps the next slice); 0 = default
   bool p2p = false;           // RCCL exchange as grouped ncclSend/ncclRecv, not ncclAllToAllv
   bool peer = false;          // exchange by direct stores into the owners' buffers
   bool peer_ready = false;    // peer tables set up
@@ -438,6 +438,11 @@ void plan_fetch(lsb_ctx* c, Rank& r) {
 // recv_counts[s] at q).
 int64_t part(int64_t n, int j, int slices) { return n * j / slices; }
 
+// Slices of an exchange: the option, else 4 per exchange digit, or 8 for the
+// whole-key exchange, whose one all-to-all carries every record: its last
+// slice's merge (ceil(log2 P) levels) is the tail after the wire goes quiet.
+int slices_of(const lsb_ctx* c) { return c->slices > 0 ? c->slices : (c->bits == 64 ? 8 : 4); }
+
 // Everything after this on r.stream waits for r.pstream's work so far.
 int join_place(Rank& r) {
   HIP_TRY(hipEventRecord(r.pdone, r.pstream));
@@ -477,8 +482,8 @@ int place_slice(lsb_ctx* c, Rank& r, int shift, int j) {
   HIP_TRY(hipStreamWaitEvent(r.pstream, r.pevent, 0));
   for (int s = 0; s < c->P; ++s) {
     if (s == r.rank) continue;
-    const int64_t lo = part(r.recv_counts[s], j, c->slices);
-    const int64_t hi = part(r.recv_counts[s], j + 1, c->slices);
+    const int64_t lo = part(r.recv_counts[s], j, slices_of(c));
+    const int64_t hi = part(r.recv_counts[s], j + 1, slices_of(c));
     LSB_TRY(place_range(c, r, shift, s, r.R + r.recv_displs[s] + lo, r.recv_displs[s] + lo, hi - lo));
   }
   return LSB_OK;
@@ -517,14 +522,14 @@ int exchange_loopback(lsb_ctx* c, int digit) {
   for (Rank& r : c->ranks) LSB_TRY(place_self(c, r, shift));
   // all-to-all-v, slice by slice: part j of segment q of rank s's
   // digit-ordered A -> rank q's R.
-  for (int j = 0; j < c->slices; ++j) {
+  for (int j = 0; j < slices_of(c); ++j) {
     for (Rank& q : c->ranks) {
       Timer t(c, &q, LSB_K_EXCHANGE);
       HIP_TRY(hipSetDevice(q.dev));
       for (Rank& s : c->ranks) {
         if (s.rank == q.rank) continue;
         const int64_t cnt = s.send_counts[q.rank];
-        const int64_t lo = part(cnt, j, c->slices), hi = part(cnt, j + 1, c->slices);
+        const int64_t lo = part(cnt, j, slices_of(c)), hi = part(cnt, j + 1, slices_of(c));
         if (hi <= lo) continue;
         HIP_TRY(hipMemcpyAsync(q.R + q.recv_displs[s.rank] + lo, s.A + s.send_displs[q.rank] + lo,
                                (size_t)(hi - lo) * sizeof(Elem), hipMemcpyDefault, q.stream));
@@ -761,14 +766,14 @@ int exchange_rccl(lsb_ctx* c, int digit) {
   // mpi/mpi_lsbsort.cpp:316-324), in uint64 units; the self entry is 0
   // because the self segment was placed straight out of A.
   std::vector<size_t> sc(P), sd(P), rc(P), rdp(P);
-  for (int j = 0; j < c->slices; ++j) {
+  for (int j = 0; j < slices_of(c); ++j) {
     {
       Timer t(c, &r, LSB_K_EXCHANGE);
       for (int q = 0; q < P; ++q) {
-        const int64_t slo = part(r.send_counts[q], j, c->slices);
-        const int64_t shi = part(r.send_counts[q], j + 1, c->slices);
-        const int64_t rlo = part(r.recv_counts[q], j, c->slices);
-        const int64_t rhi = part(r.recv_counts[q], j + 1, c->slices);
+        const int64_t slo = part(r.send_counts[q], j, slices_of(c));
+        const int64_t shi = part(r.send_counts[q], j + 1, slices_of(c));
+        const int64_t rlo = part(r.recv_counts[q], j, slices_of(c));
+        const int64_t rhi = part(r.recv_counts[q], j + 1, slices_of(c));
         sc[q] = q == me ? 0 : (size_t)(shi - slo) * 2;
         rc[q] = q == me ? 0 : (size_t)(rhi - rlo) * 2;
         sd[q] = (size_t)(r.send_displs[q] + slo) * 2;
@@ -1162,7 +1167,7 @@ int merge_slice_async(lsb_ctx* c, Rank& r, const MergeGeom& g, int j, Elem* F) {
 
 int exchange_merge(lsb_ctx* c) {
   const int P = c->P;
-  const MergeGeom g = merge_geometry(c->n, P, c->slices);
+  const MergeGeom g = merge_geometry(c->n, P, slices_of(c));
   const int Q = (int)g.target.size();
   const size_t K = lsb::kSplitCands, K1 = g.pos.size();
   for (Rank& r : c->ranks) LSB_TRY(merge_ensure(c, r, g));

@@ -72,7 +72,7 @@ typedef struct lsb_ctx lsb_ctx_t;
 #define LSB_OPT_FORCE_EXCHANGE  1  /* 1: run the exchange path even when P == 1 */
 #define LSB_OPT_SKIP_CONSTANT_DIGITS 2  /* 1 (default): lsb_sort skips every digit after
                                            the first on which all keys agree */
-#define LSB_OPT_EXCHANGE_SLICES 3  /* 1..64 (default 4): the all-to-all of a pass is cut into
+#define LSB_OPT_EXCHANGE_SLICES 3  /* 1..64 (default 4; 8 for radix_bits = 64): the all-to-all of a pass is cut into
                                       this many groups; each slice is placed while the next
                                       is in flight */
 #define LSB_OPT_EXCHANGE_P2P    4  /* RCCL contexts: 0 (default) ncclAllToAllv per slice,

@@ -63,6 +63,17 @@ def test_ragged_and_tiny(lsb_built, oracle_mod, n, P):
     assert np.array_equal(out, oracle_mod.stable_sort(a))
 
 
+@pytest.mark.parametrize("slices", [1, 3, 16, 64])
+@pytest.mark.parametrize("P", [2, 7, 8])
+def test_slices(lsb_built, oracle_mod, slices, P):
+    """Owner blocks cut into S sub-blocks (default 8), each merged while the next
+    is on the wire; P * S beyond kMergeMaxCuts = 512 is capped."""
+    rng = np.random.default_rng(slices * 13 + P)
+    a = _dist("zipf" if slices % 2 else "hot_bucket", 150_007, rng)
+    out, _, ok = _sort(lsb_built, a, P, OPT_EXCHANGE_SLICES=slices)
+    assert np.array_equal(out, oracle_mod.stable_sort(a)) and ok
+
+
 def test_one_source_owns_everything(lsb_built, oracle_mod):
     """Rank 0 holds all the small keys: every other owner receives one run."""
     n, P = 40_000, 4
