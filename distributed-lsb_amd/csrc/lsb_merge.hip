@@ -34,6 +34,8 @@
 namespace lsb {
 namespace {
 
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+
 __device__ __forceinline__ uint64_t key_at(const Elem* p, int64_t i) {
   return reinterpret_cast<const uint64_t*>(p)[2 * i];
 }
@@ -162,6 +164,30 @@ __global__ __launch_bounds__(256) void k_merge_path(MergeLevel L, int64_t* __res
 constexpr int kMergeBlock = 256;
 constexpr int kMergeIpt = kMergeTile / kMergeBlock;  // 8 outputs per thread
 
+// Step 3 of k_merge2: output x of the tile = input record idx[x] (a-range
+// first, then the b-range), gathered and stored by consecutive lanes.  Every
+// lane issues all its loads before its first store (a lane past the end of a
+// partial tile reloads the tile's last output and stores nothing), so the
+// loads stay in flight together instead of waiting one by one.  Nontemporal
+// stores: the output is read again only by the next level, milliseconds
+// later; L2 is left to the gather's re-reads.
+__device__ __forceinline__ void write_out(const Elem* __restrict__ a, const Elem* __restrict__ b,
+                                          Elem* __restrict__ out, int64_t i0, int64_t j0, int ta,
+                                          int nt, int64_t d0, const uint16_t* idx, int t) {
+  u64x2 r[kMergeIpt];
+#pragma unroll
+  for (int k = 0; k < kMergeIpt; ++k) {
+    const int x = t + k * kMergeBlock;
+    const int s = idx[x < nt ? x : nt - 1];
+    r[k] = *reinterpret_cast<const u64x2*>(s < ta ? a + (i0 + s) : b + (j0 + (s - ta)));
+  }
+#pragma unroll
+  for (int k = 0; k < kMergeIpt; ++k) {
+    const int x = t + k * kMergeBlock;
+    if (x < nt) __builtin_nontemporal_store(r[k], reinterpret_cast<u64x2*>(out + (d0 + x)));
+  }
+}
+
 // Persistent: workgroup w merges tiles w, w + grid, ... of the whole level
 // (every pair; 3 workgroups per CU, 20 KiB of LDS each, so RCCL's kernel,
 // 37 KiB of LDS, still fits on every CU while a level runs beside an
@@ -172,8 +198,8 @@ constexpr int kMergeIpt = kMergeTile / kMergeBlock;  // 8 outputs per thread
 //      tile, then a sequential merge that writes the source index of every
 //      output;
 //   3. output x of the tile = record idx[x] of the tile's input, loaded
-//      again (its line was fetched by step 1 and is still in L2) and stored
-//      by consecutive lanes: whole 128-byte lines.
+//      again (its line was fetched by step 1, mostly still in L2) and
+//      stored nontemporally by consecutive lanes: whole 128-byte lines.
 // tools/kbench/merge2.hip: keys-only staging streams at 5.2 TB/s (a plain
 // tile copy through LDS: 5.1), the full 16-byte records staged in LDS at
 // 2.5 TB/s (2 WG/CU) to 3.7 TB/s (4 WG/CU).  A pair with nb = 0 is a copy
@@ -241,16 +267,7 @@ __global__ __launch_bounds__(kMergeBlock) void k_merge2(MergeLevel L, const int6
     __syncthreads();
 
     // 3. gather the records in output order and write them out
-#pragma unroll
-    for (int k = 0; k < kMergeIpt; ++k) {
-      const int x = t + k * kMergeBlock;
-      if (x < nt) {
-        const int s = idx[x];
-        const Elem* src = s < ta ? a + (i0 + s) : b + (j0 + (s - ta));
-        LSB_MERGE_ASSERT(d0 + x < n);
-        *reinterpret_cast<ulonglong2*>(out + (d0 + x)) = *reinterpret_cast<const ulonglong2*>(src);
-      }
-    }
+    write_out(a, b, out, i0, j0, ta, nt, d0, idx, t);
     __syncthreads();  // the tile's LDS is reused
   }
 }

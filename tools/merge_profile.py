@@ -25,10 +25,13 @@ def main():
     ap.add_argument("--bits", type=int, default=64)
     ap.add_argument("--dist", default="uniform")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--slices", type=int, default=0, help="LSB_OPT_EXCHANGE_SLICES (0: default)")
     a = ap.parse_args()
     n = a.ranks * a.n_per_rank
     with lsbsort.World(n, ranks=a.ranks, radix_bits=a.bits) as w:
         w.set_timing(True)
+        if a.slices:
+            w.set_option(lsbsort.OPT_EXCHANGE_SLICES, a.slices)
         for rep in range(a.reps + 1):
             w.generate(a.dist)
             w.reset_kernel_stats()
