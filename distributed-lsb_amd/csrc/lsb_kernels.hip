@@ -888,9 +888,11 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
       const uint32_t d = (uint32_t)(v.key >> shift) & (kBuckets - 1);
       const int64_t g = delta[d] + j;
       LSB_DASSERT(g >= 0 && g < m);
-      // In range by construction; the check keeps a look-back that gave up
-      // (err set, output reported invalid) from storing outside `out`.
-      if ((uint64_t)g < (uint64_t)m) store_elem(out + g, v);
+      // In range by construction.  The clamp keeps a look-back that gave up
+      // (err set, output reported invalid) from storing outside `out`; a
+      // clamp, not a branch: the conditional store cost 6 % of the sort.
+      const uint64_t gs = (uint64_t)g < (uint64_t)(m - 1) ? (uint64_t)g : (uint64_t)(m - 1);
+      store_elem(out + gs, v);
       if (NEXT) {
         const uint32_t c = cut[d];
         const uint32_t xs = (uint32_t)j >= (c & 0xFFFFu) ? (c >> 24) : ((c >> 16) & 0xFFu);
