@@ -166,9 +166,8 @@ constexpr int kMergeIpt = kMergeTile / kMergeBlock;  // 8 outputs per thread
 
 // Step 3 of k_merge2: output x of the tile = input record idx[x] (a-range
 // first, then the b-range), gathered and stored by consecutive lanes.  Every
-// lane issues all its loads before its first store (a lane past the end of a
-// partial tile reloads the tile's last output and stores nothing), so the
-// loads stay in flight together instead of waiting one by one.  Nontemporal
+// lane issues all its loads before its first store, so the loads stay in
+// flight together instead of waiting one by one.  Nontemporal
 // stores: the output is read again only by the next level, milliseconds
 // later; L2 is left to the gather's re-reads.
 __device__ __forceinline__ void write_out(const Elem* __restrict__ a, const Elem* __restrict__ b,
@@ -181,10 +180,13 @@ __device__ __forceinline__ void write_out(const Elem* __restrict__ a, const Elem
     const int s = idx[x < nt ? x : nt - 1];
     r[k] = *reinterpret_cast<const u64x2*>(s < ta ? a + (i0 + s) : b + (j0 + (s - ta)));
   }
+  // No branch around the stores (a masked store cost k_onesweep 6 %): a lane
+  // past the end of a partial tile holds output nt - 1 and stores that same
+  // value again, to the same place.
 #pragma unroll
   for (int k = 0; k < kMergeIpt; ++k) {
     const int x = t + k * kMergeBlock;
-    if (x < nt) __builtin_nontemporal_store(r[k], reinterpret_cast<u64x2*>(out + (d0 + x)));
+    __builtin_nontemporal_store(r[k], reinterpret_cast<u64x2*>(out + (d0 + (x < nt ? x : nt - 1))));
   }
 }
 
