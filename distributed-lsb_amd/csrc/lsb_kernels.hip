@@ -126,6 +126,37 @@ __device__ __forceinline__ T wave_inclusive_scan(T v) {
   return v;
 }
 
+#ifndef LSB_NO_DPP
+// 32-bit form on DPP row shifts and row broadcasts (the generic form's
+// __shfl_up is one ds_bpermute round trip per step).  Every lane active.
+template <>
+__device__ __forceinline__ uint32_t wave_inclusive_scan<uint32_t>(uint32_t v) {
+  const uint32_t lane = lane_id(), rl = lane & 15u;
+  uint32_t t;
+  t = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  if (rl >= 1) v += t;
+  t = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  if (rl >= 2) v += t;
+  t = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  if (rl >= 4) v += t;
+  t = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  if (rl >= 8) v += t;
+  t = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x142, 0xf, 0xf, false);  // row_bcast:15
+  if ((lane & 31u) >= 16) v += t;
+  t = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x143, 0xf, 0xf, false);  // row_bcast:31
+  if (lane >= 32) v += t;
+  return v;
+}
+#endif
+
+// The value of the neighbouring lane t ^ 1 (DPP quad_perm [1,0,3,2]).
+__device__ __forceinline__ uint32_t pair_swap(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint64_t pair_swap(uint64_t v) {
+  return ((uint64_t)pair_swap((uint32_t)(v >> 32)) << 32) | pair_swap((uint32_t)v);
+}
+
 // Exclusive scan over the whole workgroup (every thread must call it).
 // `tmp` needs BLOCK/64 entries.  *total receives the block sum.
 template <int BLOCK, typename T>
@@ -813,7 +844,11 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
       wcnt[ww][t] = cnt;
       cnt += v;
     }
+#ifdef LSB_NO_DPP
     const uint32_t cnt_b = __shfl_down(cnt, 1, 64);
+#else
+    const uint32_t cnt_b = pair_swap(cnt);  // even lanes: lane t + 1's count
+#endif
     if (even) {
       const uint32_t tg = head ? tag_pre : tag_agg;
       __builtin_amdgcn_raw_buffer_store_b128(v4u{cnt, tg, cnt_b, tg}, rs, my_off, 0, 16);
@@ -858,7 +893,11 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
       __builtin_amdgcn_raw_buffer_store_b128(
           v4u{(uint32_t)(ea + cnt), tag_pre, (uint32_t)(eb + cnt_b), tag_pre}, rs, my_off, 0, 16);
     }
+#ifdef LSB_NO_DPP
     const uint64_t eb_left = __shfl_up(eb, 1, 64);
+#else
+    const uint64_t eb_left = pair_swap(eb);  // odd lanes: lane t - 1's sum
+#endif
     const uint64_t excl = even ? ea : eb_left;
     const int64_t R = (int64_t)(base + excl);  // first output slot of the run
     delta[t] = R - (int64_t)lstart;

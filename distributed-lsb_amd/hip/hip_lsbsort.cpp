@@ -15,7 +15,8 @@
 //              `mpirun -n P mpi_lsbsort` on one GPU.
 //   --json     also print one machine-readable line.
 //   --radix-bits 8|16|64  exchange digit width (local passes are always 8-bit);
-//              64: local sort, one all-to-all, merge of the P runs
+//              64: local sort, one all-to-all, merge of the P runs (the default
+//              with --gpus P > 1, as in bench.py; 8 otherwise)
 //   --dist uniform|zipf [--zipf-s S]   key distribution of the same pcg64 stream
 //   --exchange alltoallv|p2p|peer  element exchange (default RCCL AllToAllv in
 //              slices; grouped Send/Recv; direct peer stores, the shmem_putmem form)
@@ -44,7 +45,7 @@ struct Options {
   int ranks = 1;
   int device = 0;
   bool json = false;
-  int radix_bits = 8;
+  int radix_bits = 0;        // --radix-bits (0: 64 with --gpus > 1, else 8)
   int dist = LSB_DIST_UNIFORM;
   double zipf_s = 1.1;
   int exchange_option = -1;  // --exchange: LSB_OPT_EXCHANGE_P2P / _PEER, or -1 (AllToAllv)
@@ -246,6 +247,7 @@ int main(int argc, char* argv[]) {
     }
   }
   if (!o.verify_set) o.verify = (o.n < 128LL * 1024 * 1024);
+  if (o.radix_bits == 0) o.radix_bits = o.gpus > 1 ? 64 : 8;
   if (o.n < 0 || o.ranks < 1 || o.gpus < 0) {
     fprintf(stderr, "invalid arguments\n");
     return 2;
