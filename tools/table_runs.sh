@@ -1,0 +1,21 @@
+#!/bin/bash
+# The DESIGN.md §4 bench table on one box: C2 default, reduce-then-scan,
+# Zipf keys, 16-bit digits, 2^32 records (bench.py lines in gpurun_out/table.log).
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+cd $R
+: > gpurun_out/table.log
+for args in "" "--passes reduce-scan" "--dist zipf" "--radix-bits 16" "--n-per-gpu 4294967296 --steps 3 --warmup 1"; do
+  echo "args: $args" >> gpurun_out/table.log
+  timeout -k 10 300 python -u bench.py --no-cpu-baseline $args >> gpurun_out/table.log 2>&1 || exit 1
+done
+python3 - <<'PY'
+import json
+for line in open("gpurun_out/table.log"):
+    if line.startswith("args:"):
+        a = line.strip()
+    elif line.startswith("{"):
+        d = json.loads(line)
+        r = d["roofline"]
+        print(f"{a:50s} {d['value']:10.1f} Melem/s {d['ms_per_step']:8.2f} ms  {r['kernel']} {r['avg_launch_ms']:.3f} ms frac {r['frac']:.3f}")
+PY
