@@ -18,6 +18,7 @@
 //     tile-sorted order, so each bucket's run leaves the CU as contiguous
 //     16-byte stores from consecutive lanes.
 #include "lsb_kernels.h"
+#include <type_traits>
 
 // Debug build (make debug, -DLSB_DEBUG): device-side bounds asserts on every
 // scattered store.  A failing assert prints and traps the kernel.
@@ -742,6 +743,12 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
   }
   uint64_t all;
   const uint64_t bstart = block_exclusive_scan<BLOCK>(tot, scan64, &all);
+  // Skewed digit (one bucket holds more than 1/32 of the records, e.g. Zipf
+  // keys): runs of equal next digits are then long, and 64 lanes adding to
+  // one LDS counter serialise.  Such launches add once per wave-instruction
+  // whose records share a slot; uniform keys keep the plain add (the check
+  // costs them 5.7 %, tools/ab.sh).  Launch-uniform.
+  const bool skewed = NEXT && __syncthreads_or(tot > (uint64_t)(m >> 5)) != 0;
   if (NEXT)
     for (int i = t; i < kSub * kBuckets; i += BLOCK) nh[i] = 0;
 
@@ -922,23 +929,42 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
     OS_MARK(3);  // stage + look-back
     if (t == 0) grab(nxt_tile, nxt_sub);  // in flight during the writes
 
-    for (int j = t; j < nvalid; j += BLOCK) {
-      const Elem v = stage[j];
-      const uint32_t d = (uint32_t)(v.key >> shift) & (kBuckets - 1);
-      const int64_t g = delta[d] + j;
-      LSB_DASSERT(g >= 0 && g < m);
-      // In range by construction.  The clamp keeps a look-back that gave up
-      // (err set, output reported invalid) from storing outside `out`; a
-      // clamp, not a branch: the conditional store cost 6 % of the sort.
-      const uint64_t gs = (uint64_t)g < (uint64_t)(m - 1) ? (uint64_t)g : (uint64_t)(m - 1);
-      store_elem(out + gs, v);
-      if (NEXT) {
-        const uint32_t c = cut[d];
-        const uint32_t xs = (uint32_t)j >= (c & 0xFFFFu) ? (c >> 24) : ((c >> 16) & 0xFFu);
-        const uint32_t dn = (uint32_t)(v.key >> next_shift) & (kBuckets - 1);
-        atomicAdd(&nh[xs * kBuckets + dn], 1u);
+    // The loop is instantiated twice (the launch-uniform `skewed` picks one
+    // outside it): a per-record branch on it cost uniform keys 2.4 %.
+    auto write_out = [&](auto skew_tag) {
+      constexpr bool kSkew = decltype(skew_tag)::value;
+      for (int j = t; j < nvalid; j += BLOCK) {
+        const Elem v = stage[j];
+        const uint32_t d = (uint32_t)(v.key >> shift) & (kBuckets - 1);
+        const int64_t g = delta[d] + j;
+        LSB_DASSERT(g >= 0 && g < m);
+        // In range by construction.  The clamp keeps a look-back that gave up
+        // (err set, output reported invalid) from storing outside `out`; a
+        // clamp, not a branch: the conditional store cost 6 % of the sort.
+        const uint64_t gs = (uint64_t)g < (uint64_t)(m - 1) ? (uint64_t)g : (uint64_t)(m - 1);
+        store_elem(out + gs, v);
+        if (NEXT) {
+          const uint32_t c = cut[d];
+          const uint32_t xs = (uint32_t)j >= (c & 0xFFFFu) ? (c >> 24) : ((c >> 16) & 0xFFu);
+          const uint32_t dn = (uint32_t)(v.key >> next_shift) & (kBuckets - 1);
+          const uint32_t slot = xs * kBuckets + dn;
+          if (kSkew) {
+            // One add per wave-instruction whose records share the slot.
+            const uint32_t s0 = __builtin_amdgcn_readfirstlane(slot);
+            const uint64_t act = __ballot(1);
+            if (__ballot(slot == s0) == act) {
+              if (mbcnt(act) == 0) atomicAdd(&nh[s0], (uint32_t)__popcll(act));
+            } else {
+              atomicAdd(&nh[slot], 1u);
+            }
+          } else {
+            atomicAdd(&nh[slot], 1u);
+          }
+        }
       }
-    }
+    };
+    if (skewed) write_out(std::true_type{});
+    else write_out(std::false_type{});
     __syncthreads();
     OS_MARK(4);  // write
   }
