@@ -4,8 +4,8 @@
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-A step is one full sort (mySort: 8 passes of 8-bit digits over 64-bit keys)
-of 2^30 16-byte records per GPU (weak scaling: n = N * 2^30), generated on
+A step is one full sort (mySort: 8 local passes of 8-bit digits over 64-bit
+keys) of 2^30 16-byte records per GPU (weak scaling: n = N * 2^30), generated on
 device with the reference's PCG64 input (seed = rank, val = global index;
 mpi/mpi_lsbsort.cpp:650-656) before every step, outside the timed window —
 the reference times the sort only (mpi/mpi_lsbsort.cpp:688-699).  Each step
@@ -16,11 +16,15 @@ the max over ranks.  The result of the last step is verified on device
 Multi-GPU: one process per GPU (RANK / WORLD_SIZE / LOCAL_RANK from the
 environment).  torch.distributed (gloo, CPU) only ships the RCCL unique id
 and reduces timings; the data path is the library's own RCCL communicator.
+The default exchange at N > 1 is the whole key (--radix-bits 64: local sort,
+one sliced all-to-all, merge); --radix-bits 16 / 8 exchange
+once per digit, as the reference does.
 
-The JSON line carries the roofline of the dominant kernel (k_scatter, 32
-algorithmic bytes per record per launch, timed with HIP events on the
-library's stream) and, on rank 0 at N = 1, a CPU baseline: the reference's
-own mpi_lsbsort (oracle/_ref, built from /root/reference) on the host cores.
+The JSON line carries the roofline of the dominant kernel (k_onesweep, or
+k_scatter with --passes reduce-scan: 32 algorithmic bytes per record per
+launch, timed with HIP events on the library's stream) and, on rank 0 at
+N = 1, a CPU baseline: the reference's own mpi_lsbsort (oracle/_ref, built
+from /root/reference) on the host cores.
 """
 import argparse
 import json
