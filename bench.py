@@ -377,6 +377,14 @@ def main():
         "roofline": roof,
         "sort_hbm_frac": round(sort_gbs / HBM_PEAK_GBS, 4),
         "kernel_ms_per_step": {k: round(v[1] / a.steps, 3) for k, v in stats.items()},
+        "kernel_ms_per_step_legend": {
+            "upsweep": "count read (k_subhist once per sort, or k_upsweep per pass)",
+            "scan": "chunk scan (k_scan, reduce-then-scan only)",
+            "scatter": "local passes (k_onesweep, or k_scatter)",
+            "exchange": "exchange on the rank's stream: splitter search + all-to-all (whole key) "
+                        "or counts all-gather + plan + all-to-all (per digit); includes wire time",
+            "place": "placement stream: merge of the received runs (whole key) or k_place",
+            "sort": "the whole sort, per rank"},
         "verified": verified,
         "vs_baseline_basis": "MPI mpi_lsbsort 830 M elem/s (64 nodes x 128 cores, n=2^36; BASELINE.md §1)",
     }
