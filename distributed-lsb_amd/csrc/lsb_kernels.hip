@@ -111,6 +111,15 @@ __device__ __forceinline__ Elem load_elem(const Elem* p) {
   return Elem{v.x, v.y};
 }
 
+// Streaming load: the record is read once per pass, so its line is marked
+// for early eviction and L2 keeps room for the run-boundary lines the next
+// tile completes (k_onesweep: -1...-5 % per sort, tools/ab.sh).
+__device__ __forceinline__ Elem load_elem_nt(const Elem* p) {
+  typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+  const u64x2 v = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(p));
+  return Elem{v.x, v.y};
+}
+
 __device__ __forceinline__ void store_elem(Elem* p, const Elem& e) {
   *reinterpret_cast<ulonglong2*>(p) = make_ulonglong2(e.key, e.val);
 }
@@ -811,7 +820,7 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
       const int li = wbase + i * 64;
-      e[i] = li < nvalid ? load_elem(in + tb + li) : Elem{0ull, 0ull};
+      e[i] = li < nvalid ? load_elem_nt(in + tb + li) : Elem{0ull, 0ull};
     }
     // Status rows of this sub-array through one buffer descriptor (byte
     // offsets < 2^31); the even lane of a pair publishes and polls buckets
