@@ -265,7 +265,7 @@ __global__ __launch_bounds__(BLOCK) void k_upsweep(const Elem* __restrict__ A, i
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
       const int64_t idx = tb + (int64_t)i * BLOCK + threadIdx.x;
-      k[i] = idx < end ? keys[2 * idx] : 0ull;
+      k[i] = idx < end ? __builtin_nontemporal_load(keys + 2 * idx) : 0ull;  // streaming
     }
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
@@ -655,7 +655,7 @@ __global__ __launch_bounds__(BLOCK) void k_subhist(const Elem* __restrict__ A, i
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
       const int64_t idx = tb + (int64_t)i * BLOCK + threadIdx.x;
-      k[i] = idx < end ? keys[2 * idx] : 0ull;
+      k[i] = idx < end ? __builtin_nontemporal_load(keys + 2 * idx) : 0ull;  // streaming
     }
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
