@@ -16,15 +16,19 @@ the max over ranks.  The result of the last step is verified on device
 Multi-GPU: one process per GPU (RANK / WORLD_SIZE / LOCAL_RANK from the
 environment).  torch.distributed (gloo, CPU) only ships the RCCL unique id
 and reduces timings; the data path is the library's own RCCL communicator.
-The default exchange at N > 1 is the whole key (--radix-bits 64: local sort,
-one sliced all-to-all, merge); --radix-bits 16 / 8 exchange
-once per digit, as the reference does.
+At N > 1 the headline is the reference's own structure (BASELINE configs[2],
+configs[3]): per 16-bit digit (the reference's RADIX 16) an RCCL AllGather
+of the counts and an RCCL AllToAllv of the records (--radix-bits 16;
+--radix-bits 8 exchanges per 8-bit digit).  The whole-key exchange (local
+sort, one sliced all-to-all, merge) is timed after it and
+reported as an extra key (whole_key_melem_s), not as `value`.
 
 The JSON line carries the roofline of the dominant kernel (k_onesweep, or
-k_scatter with --passes reduce-scan: 32 algorithmic bytes per record per
-launch, timed with HIP events on the library's stream) and, on rank 0 at
-N = 1, a CPU baseline: the reference's own mpi_lsbsort (oracle/_ref, built
-from /root/reference) on the host cores.
+k_scatter: 32 algorithmic bytes per record per launch, timed with HIP events
+on the library's stream), its HBM traffic measured in this run (N = 1: two
+rocprofv3 --pmc passes, FETCH_SIZE and WRITE_SIZE, over one sort of the same
+workload), and, on rank 0, a CPU baseline: the reference's own mpi_lsbsort
+(oracle/_ref, built from /root/reference) on the host's cores, median of 3.
 """
 import argparse
 import json
@@ -54,12 +58,18 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--n-per-gpu", type=int, default=1 << 30)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=1 << 27,
-                    help="records the CPU baseline sorts (bounded sample)")
+    ap.add_argument("--cpu-n", type=int, default=0,
+                    help="records the CPU baseline sorts (default: the GPU run's n, capped by host "
+                         "memory and a ~20 s per-run budget, as a power of two)")
+    ap.add_argument("--no-traffic", action="store_true",
+                    help="skip the rocprofv3 --pmc passes that measure the dominant kernel's HBM bytes")
+    ap.add_argument("--no-whole-key", action="store_true",
+                    help="N > 1: skip the extra whole-key exchange timing")
+    ap.add_argument("--probe", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--radix-bits", type=int, default=0, choices=(0, 8, 16, 64),
                     help="exchange digit width: 8 or 16 (one all-to-all per digit), or 64 (the "
-                         "whole key: local sort, ONE all-to-all, merge); default 8 on 1 GPU, 64 on "
+                         "whole key: local sort, ONE all-to-all, merge); default 8 on 1 GPU, 16 on "
                          ">1 GPU; local passes are 8-bit either way")
     ap.add_argument("--dist", choices=("uniform", "zipf"), default="uniform")
     ap.add_argument("--transport", choices=("rccl", "gloo"), default="rccl",
@@ -194,50 +204,127 @@ def device_sync():
     torch.cuda.synchronize(_TORCH_DEV)
 
 
-def load_traffic(workload, kernel):
-    """Per-launch HBM bytes of the dominant kernel from the committed rocprofv3 PMC summary."""
-    path = os.path.join(ROOT, "profiles", "pmc_scatter.json")
+def measure_traffic(a, kernel, elems):
+    """HBM bytes per launch of `kernel`, measured now: two rocprofv3 --pmc
+    passes (FETCH_SIZE, then WRITE_SIZE: they cannot share a pass) over one
+    sort of the same workload (this script with --probe), combined as
+    MI355X_MICROARCH.md §HBM prescribes for gfx950: 2 * FETCH_SIZE (it counts
+    half of a 16 B/lane stream) + WRITE_SIZE, in KB.  None when rocprofv3 is
+    absent or a pass fails."""
+    import collections
+    import csv
+    import tempfile
+    prof = shutil.which("rocprofv3")
+    if not prof:
+        return None, "rocprofv3 not found"
+    probe = [sys.executable, os.path.abspath(__file__), "--probe", "--n-per-gpu", str(a.n_per_gpu),
+             "--dist", a.dist, "--zipf-s", str(a.zipf_s), "--passes", a.passes,
+             "--radix-bits", str(a.radix_bits or 8)]
+    env = dict(os.environ, TMPDIR="/tmp")
+    vals = {}
+    with tempfile.TemporaryDirectory(dir="/tmp") as tmp:
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            out = os.path.join(tmp, counter)
+            cmd = ["timeout", "-s", "KILL", "120", prof, "--kernel-trace", "--pmc", counter,
+                   "--kernel-include-regex", kernel, "--output-format", "csv", "-d", out, "-o", "run",
+                   "--"] + probe
+            try:
+                subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, timeout=150, check=True)
+            except (subprocess.SubprocessError, OSError) as e:
+                return None, f"rocprofv3 --pmc {counter} failed: {type(e).__name__}"
+            per = collections.defaultdict(list)
+            for root, _, files in os.walk(out):
+                for f in files:
+                    if f.endswith("counter_collection.csv"):
+                        for r in csv.DictReader(open(os.path.join(root, f))):
+                            if r["Counter_Name"] == counter and kernel in r["Kernel_Name"]:
+                                per[r.get("Dispatch_Id", len(per))].append(float(r["Counter_Value"]))
+            if not per:
+                return None, f"no {counter} rows for {kernel}"
+            vals[counter] = sum(sum(v) for v in per.values()) / len(per)
+    hbm = (2 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024
+    return hbm, (f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes in this run, one sort, {kernel} "
+                 f"launches averaged; hbm = (2*FETCH_SIZE + WRITE_SIZE) KB * 1024 "
+                 f"(algorithmic {SCATTER_BYTES_PER_ELEM * elems:.4g} B per launch)")
+
+
+def host_cores():
+    """Core counts of this host: nproc, lscpu's physical cores, and this
+    job's CPU share (OMP_NUM_THREADS as the GPU pool sets it per job, else the
+    cgroup quota, else the affinity mask)."""
+    total = os.cpu_count() or 1
     try:
-        with open(path) as f:
-            d = json.load(f)
-        if d.get("workload") == workload and d.get("kernel", "k_scatter").split("<")[0] == kernel:
-            return d.get("hbm_bytes_per_launch")
+        rows = subprocess.run(["lscpu", "-p=CORE,SOCKET"], capture_output=True, text=True,
+                              timeout=10).stdout.splitlines()
+        physical = len({r for r in rows if r and not r.startswith("#")}) or None
+    except (subprocess.SubprocessError, OSError):
+        physical = None
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = total
+    share, basis = affinity, "affinity mask"
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            share, basis = min(share, max(1, int(int(q) / int(per)))), "cgroup cpu.max"
     except (OSError, ValueError):
         pass
-    return None
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0 and int(omp) < share:
+        share, basis = int(omp), "OMP_NUM_THREADS (the job's CPU share)"
+    return {"nproc": total, "physical": physical, "affinity": affinity, "share": share,
+            "share_basis": basis}
 
 
-def cpu_baseline(sample):
-    """The reference's own MPI sort on this host's cores (bounded sample)."""
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    cores = max(1, min(cores, 16))
+def cpu_baseline(gpu_n, cpu_n=0, runs=3):
+    """The reference's own MPI sort (mpi/mpi_lsbsort.cpp, oracle/_ref) on this
+    host, per BASELINE.md §4: one rank per core of the job's CPU share (at
+    least 5 ranks), n = the GPU run's n or the largest power of two that fits
+    ~80 B per record of host memory and a ~20 s per-run budget, the median of
+    `runs` runs of its sort-only window (mpi/mpi_lsbsort.cpp:688-699)."""
+    cores = host_cores()
+    ranks = max(5, cores["share"])
     ref = os.path.join(ROOT, "oracle", "_ref", "mpi_lsbsort")
     mpirun = shutil.which("mpirun") or "/opt/conda/bin/mpirun"
-    if os.path.exists(ref) and os.path.exists(mpirun):
-        cmd = [mpirun, "-n", str(cores), ref, "--n", str(sample), "--no-verify"]
+    if not (os.path.exists(ref) and os.path.exists(mpirun)):
+        return None
+    try:
+        import psutil
+        avail = psutil.virtual_memory().available
+    except Exception:
+        avail = 32 << 30
+    if cpu_n:
+        n, why = cpu_n, "requested"
+    else:
+        mem_cap = min(avail * 0.6, 200 << 30) / 80
+        time_cap = 20 * 4e6 * ranks  # the reference sorts ~4-6 M records/s per rank (BASELINE.md §2)
+        n, why = gpu_n, "the GPU run's n"
+        if n > mem_cap or n > time_cap:
+            n = 1 << int(min(mem_cap, time_cap, gpu_n)).bit_length() - 1
+            why = ("largest power of two within " +
+                   ("host memory (80 B/record)" if mem_cap < time_cap else "a ~20 s per-run budget"))
+    vals = []
+    cmd = [mpirun, "-n", str(ranks), ref, "--n", str(n), "--no-verify"]
+    for _ in range(runs):
         try:
-            out = subprocess.run(cmd, capture_output=True, text=True, timeout=240, check=True).stdout
-            m = re.search(r"That's ([0-9.eE+-]+) M elements sorted / s", out)
-            if m:
-                return {"value": float(m.group(1)), "unit": "Melem/s", "cores": cores,
-                        "kind": "reference",
-                        "sample": f"mpirun -n {cores} oracle/_ref/mpi_lsbsort --n {sample} --no-verify "
-                                  "(reference mpi/mpi_lsbsort.cpp, 16-bit digits, sort-only window)"}
+            out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, check=True).stdout
         except (subprocess.SubprocessError, OSError):
-            pass
-    # fallback: the oracle's single-threaded C restatement
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle
-    n = min(sample, 1 << 24)
-    slots = oracle.generate_slots(n, 1)
-    t0 = time.perf_counter()
-    oracle.mpi_sort_slots(n, 1, slots, bits=16)
-    dt = time.perf_counter() - t0
-    return {"value": n / dt / 1e6, "unit": "Melem/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/lsb_oracle.c oracle_mpi_sort n={n} P=1 16-bit"}
+            break
+        m = re.search(r"That's ([0-9.eE+-]+) M elements sorted / s", out)
+        if not m:
+            break
+        vals.append(float(m.group(1)))
+    if not vals:
+        return None
+    med = sorted(vals)[len(vals) // 2]
+    return {"value": med, "unit": "Melem/s", "cores": ranks, "kind": "reference",
+            "n": n, "n_basis": why, "ranks": ranks, "runs": vals, "median": med,
+            "cores_total": cores["nproc"], "cores_physical": cores["physical"],
+            "cores_share": cores["share"], "cores_share_basis": cores["share_basis"],
+            "cores_used": ranks,
+            "sample": f"mpirun -n {ranks} oracle/_ref/mpi_lsbsort --n {n} --no-verify (the reference "
+                      f"mpi/mpi_lsbsort.cpp, 16-bit digits, its sort-only window), median of {len(vals)}"}
 
 
 def parallelism(N, radix, a):
@@ -255,41 +342,37 @@ def parallelism(N, radix, a):
              "peer": "direct peer stores (IPC)"}[a.exchange])
 
 
-def main():
-    a = parse()
-    d = Dist()
-    N = d.world if d.world > 1 else a.gpus
-    if d.world > 1 and a.gpus != d.world:
-        N = d.world
-    n_total = a.n_per_gpu * N
-    radix = a.radix_bits or (8 if N == 1 else 64)
-    if radix == 64 and a.exchange == "peer":
-        raise SystemExit("--exchange peer is a per-digit exchange form; use --radix-bits 8 or 16")
-    device = d.local_rank
+def make_world(a, d, N, n_total, radix):
+    """The sort context of this process: one rank of an RCCL world (N > 1),
+    one rank over gloo host collectives (--transport gloo), or one GPU."""
     if d.world > 1 and a.transport == "gloo":
         # Rehearsal: ranks may share GPUs; collectives go through gloo on the host.
         device = d.local_rank % max(1, visible_devices())
         w = lsbsort.World.rank_ops(n_total, N, d.rank, device, GlooComm(d.dist, d.world, d.rank),
                                    radix_bits=radix)
     elif d.world > 1:
+        device = d.local_rank
         uid = lsbsort.get_unique_id() if d.rank == 0 else None
         uid = d.bcast_bytes(uid)
         w = lsbsort.World.rank(n_total, N, d.rank, d.local_rank, uid, radix_bits=radix)
     else:
         if N != 1:
             raise SystemExit("multi-GPU runs are launched one process per GPU (torch.distributed.run)")
+        device = 0
         w = lsbsort.World(n_total, ranks=1, radix_bits=radix)
-    bind_device(device)
     if a.exchange == "p2p":
         w.set_option(lsbsort.OPT_EXCHANGE_P2P, 1)
-    elif a.exchange == "peer":
+    elif a.exchange == "peer" and radix != 64:
         w.set_option(lsbsort.OPT_EXCHANGE_PEER, 1)
     w.set_option(lsbsort.OPT_ONESWEEP, 1 if a.passes == "onesweep" else 0)
-    # Dominant kernel: the local pass.  Single-read passes run wherever a rank
-    # sorts its block alone: P = 1, and every rank of the whole-key exchange.
-    kernel = "k_onesweep" if ((N == 1 or radix == 64) and a.passes == "onesweep") else "k_scatter"
+    return w, device
 
-    def step(timed):
+
+def timed_sorts(w, d, a, steps, warmup):
+    """`warmup` untimed sorts, then `steps` timed ones; each step regenerates
+    the input (untimed) and times the sort between barrier + synchronize
+    brackets.  Returns (max-over-ranks total seconds, verified or None)."""
+    def step():
         w.generate(a.dist, a.zipf_s)
         w.barrier()
         device_sync()
@@ -301,21 +384,54 @@ def main():
         d.barrier()
         return time.perf_counter() - t0
 
-    for _ in range(a.warmup):
-        step(False)
+    for _ in range(warmup):
+        step()
     w.reset_kernel_stats()
     w.set_timing(True)
     total = 0.0
-    for _ in range(a.steps):
-        total += step(True)
+    for _ in range(steps):
+        total += step()
     w.set_timing(False)
-    stats = w.kernel_stats()
-    scatter_elems = w.scatter_elems()
     verified = None
     if not a.no_verify:
-        ok, bad = w.verify()
+        ok, _ = w.verify()
         verified = d.all_true(ok)
-    total = d.max(total)
+    return d.max(total), verified
+
+
+def probe(a):
+    """One sort of the workload, nothing printed: the program rocprofv3's
+    --pmc passes run (measure_traffic)."""
+    w = lsbsort.World(a.n_per_gpu, ranks=1, radix_bits=a.radix_bits or 8)
+    w.set_option(lsbsort.OPT_ONESWEEP, 1 if a.passes == "onesweep" else 0)
+    w.generate(a.dist, a.zipf_s)
+    w.my_sort()
+    w.sync()
+    w.close()
+
+
+def main():
+    a = parse()
+    if a.probe:
+        return probe(a)
+    d = Dist()
+    N = d.world if d.world > 1 else a.gpus
+    n_total = a.n_per_gpu * N
+    radix = a.radix_bits or (8 if N == 1 else 16)
+    if radix == 64 and a.exchange == "peer":
+        raise SystemExit("--exchange peer is a per-digit exchange form; use --radix-bits 8 or 16")
+    w, device = make_world(a, d, N, n_total, radix)
+    bind_device(device)
+    # Dominant kernel: the local pass.  Single-read passes run wherever a rank
+    # sorts its block alone: P = 1, and every rank of the whole-key exchange.
+    kernel = "k_onesweep" if ((N == 1 or radix == 64) and a.passes == "onesweep") else "k_scatter"
+
+    total, verified = timed_sorts(w, d, a, a.steps, a.warmup)
+    stats = w.kernel_stats()
+    scatter_elems = w.scatter_elems()
+    xcalls, xbytes, _ = w.exchange_bytes()
+    last = w.last_sort()
+    w.close()
 
     ms_per_step = total / a.steps * 1e3
     value = n_total * a.steps / total / 1e6
@@ -332,7 +448,7 @@ def main():
         cfg = "configs[2]" if a.dist == "uniform" else "configs[3]"
         workload = (f"{cfg}: sort of {N} x {size} 16-byte records block-partitioned over {N} GPUs, "
                     f"8-bit local passes, " +
-                    (f"{radix}-bit exchange digits ({64 // radix} all-to-alls)" if radix != 64 else
+                    (f"RCCL AllToAllv per {radix}-bit digit ({64 // radix} exchanges)" if radix != 64 else
                      "whole-key exchange digit (local sort, 1 all-to-all, merge of the P runs)"))
     if a.dist != "uniform":
         workload += f", zipf s={a.zipf_s} keys"
@@ -343,9 +459,15 @@ def main():
         elems_per_launch = scatter_elems / launches
         avg_s = scatter_ms / launches / 1e3
         achieved = SCATTER_BYTES_PER_ELEM * elems_per_launch / avg_s / 1e9
-        traffic = load_traffic(workload, kernel)
+        traffic, traffic_src = None, "not measured at N > 1 (rocprofv3 passes run at N = 1)"
+        if N == 1 and not a.no_traffic:
+            traffic, traffic_src = measure_traffic(a, kernel, elems_per_launch)
+        elif a.no_traffic:
+            traffic_src = "skipped (--no-traffic)"
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "traffic_ratio": round(traffic / (SCATTER_BYTES_PER_ELEM * elems_per_launch), 4)
+                if traffic else None, "traffic_source": traffic_src,
                 "kernel": kernel, "bytes_per_launch": int(SCATTER_BYTES_PER_ELEM * elems_per_launch),
                 "avg_launch_ms": round(scatter_ms / launches, 4)}
     # Algorithmic bytes of a sort: 32 B per record per scatter launch, 16 B
@@ -369,9 +491,10 @@ def main():
                  if a.dist == "uniform" else
                  f"synthetic: zipf(s={a.zipf_s}) keys drawn from the pcg64(rank) stream (build-defined, SURVEY 8d C4)"),
         "config": {"workload": workload, "n_total": n_total, "n_per_gpu": a.n_per_gpu,
-                   "local_digit_bits": 8, "local_passes": 8,
+                   "local_digit_bits": 8, "local_passes": last[0], "exchanges": last[1],
                    "pass_form": ("single-read (k_subhist once, k_onesweep per pass)" if kernel == "k_onesweep"
-                                 else "reduce-then-scan (k_upsweep, k_scan, k_scatter per pass)"), "exchange_digit_bits": radix if N > 1 else None,
+                                 else "reduce-then-scan (k_upsweep, k_scan, k_scatter per pass)"),
+                   "exchange_digit_bits": radix if N > 1 else None,
                    "record_bytes": 16, "dist": a.dist,
                    "parallelism": parallelism(N, radix, a)},
         "roofline": roof,
@@ -385,18 +508,29 @@ def main():
                         "or counts all-gather + plan + all-to-all (per digit); includes wire time",
             "place": "placement stream: merge of the received runs (whole key) or k_place",
             "sort": "the whole sort, per rank"},
+        "exchange_bytes_per_step": xbytes // a.steps if N > 1 else 0,
         "verified": verified,
         "vs_baseline_basis": "MPI mpi_lsbsort 830 M elem/s (64 nodes x 128 cores, n=2^36; BASELINE.md §1)",
+        "library": lsbsort.build_info(),
     }
-    if d.rank == 0 and N == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(a.cpu_sample)
+    if N > 1 and radix != 64 and not a.no_whole_key:
+        # The whole-key exchange (one all-to-all per sort), same input, fewer steps.
+        wk, _ = make_world(a, d, N, n_total, 64)
+        k = min(a.steps, 3)
+        wt, wv = timed_sorts(wk, d, a, k, 1)
+        wk.close()
+        out["whole_key_melem_s"] = round(n_total * k / wt / 1e6, 2)
+        out["whole_key_ms_per_step"] = round(wt / k * 1e3, 3)
+        out["whole_key_verified"] = wv
+    if d.rank == 0 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(n_total, a.cpu_n)
     elif d.rank == 0:
         out["cpu_baseline"] = None
-    w.close()
+    d.barrier()
     d.close()
     if d.rank == 0:
         print(json.dumps(out), flush=True)
-    if verified is False:
+    if verified is False or out.get("whole_key_verified") is False:
         sys.exit(1)
 
 

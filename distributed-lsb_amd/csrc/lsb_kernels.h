@@ -116,9 +116,12 @@ hipError_t launch_place(const Elem* src, Elem* out, int64_t out_len, int64_t k0,
 // records straight into its owner's receiving buffer: record i of bucket b
 // goes to global position g = base[b] + i, i.e. dst[g / per][g % per].
 // dst[q] is rank q's buffer as this process sees it; base: nb int64 scratch.
+// Each workgroup ends with a system-scope release; launch_system_acquire is
+// the owner's matching acquire (every XCD's L2) after the barrier collective.
 hipError_t launch_peer_exchange(const Elem* src, int64_t m, int shift, int nbuckets,
                                 const uint64_t* hist, int P, int me, int64_t per,
                                 Elem* const* dst, int64_t* base, hipStream_t s);
+hipError_t launch_system_acquire(hipStream_t s);
 
 // Exchange plan of rank `me` on device from the all-gathered counts
 // hist[s * nb + b] (same rule as the host planner lsb_plan_exchange):

@@ -136,7 +136,6 @@ __device__ __forceinline__ T wave_inclusive_scan(T v) {
   return v;
 }
 
-#ifndef LSB_NO_DPP
 // 32-bit form on DPP row shifts and row broadcasts (the generic form's
 // __shfl_up is one ds_bpermute round trip per step).  Every lane active.
 template <>
@@ -157,7 +156,6 @@ __device__ __forceinline__ uint32_t wave_inclusive_scan<uint32_t>(uint32_t v) {
   if (lane >= 32) v += t;
   return v;
 }
-#endif
 
 // The value of the neighbouring lane t ^ 1 (DPP quad_perm [1,0,3,2]).
 __device__ __forceinline__ uint32_t pair_swap(uint32_t v) {
@@ -589,9 +587,7 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_scatter(const Elem* __re
 // from k_subhist: one read per sort instead of one per pass.
 constexpr int kSub = kOnesweepSubs;
 constexpr uint32_t kSpinLimit = 1u << 22;  // look-back polls before giving up (seconds)
-#ifndef LSB_OS_SLEEP
-#define LSB_OS_SLEEP 1
-#endif
+constexpr int kPollSleep = 1;              // s_sleep between look-back polls (4, 16: no change)
 
 typedef __attribute__((address_space(1))) uint32_t gu32;
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
@@ -860,11 +856,7 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
       wcnt[ww][t] = cnt;
       cnt += v;
     }
-#ifdef LSB_NO_DPP
-    const uint32_t cnt_b = __shfl_down(cnt, 1, 64);
-#else
     const uint32_t cnt_b = pair_swap(cnt);  // even lanes: lane t + 1's count
-#endif
     if (even) {
       const uint32_t tg = head ? tag_pre : tag_agg;
       __builtin_amdgcn_raw_buffer_store_b128(v4u{cnt, tg, cnt_b, tg}, rs, my_off, 0, 16);
@@ -896,7 +888,7 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
           if (g.y == tag_pre) break;
           --prow;
         } else {
-          __builtin_amdgcn_s_sleep(LSB_OS_SLEEP);
+          __builtin_amdgcn_s_sleep(kPollSleep);
           if ((++spins & 1023u) == 0 &&
               (spins > kSpinLimit ||
                __hip_atomic_load((gu32*)err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)) {
@@ -909,11 +901,7 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
       __builtin_amdgcn_raw_buffer_store_b128(
           v4u{(uint32_t)(ea + cnt), tag_pre, (uint32_t)(eb + cnt_b), tag_pre}, rs, my_off, 0, 16);
     }
-#ifdef LSB_NO_DPP
-    const uint64_t eb_left = __shfl_up(eb, 1, 64);
-#else
     const uint64_t eb_left = pair_swap(eb);  // odd lanes: lane t - 1's sum
-#endif
     const uint64_t excl = even ? ea : eb_left;
     const int64_t R = (int64_t)(base + excl);  // first output slot of the run
     delta[t] = R - (int64_t)lstart;
@@ -1112,6 +1100,22 @@ __global__ __launch_bounds__(kPlaceBlock) void k_peer_scatter(const Elem* __rest
       }
     }
   }
+  // Release at system scope (shmem_putmem's completion before
+  // shmem_barrier_all, shmem/shmem_lsbsort.cpp:455-456): after the barrier
+  // every wave's stores have left it (s_waitcnt), and one system-scope
+  // release per workgroup writes back this XCD's L2 (buffer_wbl2 sc0 sc1),
+  // so stores to a peer's memory that the L2 holds reach it before the
+  // kernel ends.  The owner acquires (k_system_acquire) after the barrier
+  // collective, before its next pass reads the buffer.
+  __syncthreads();
+  if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+}
+
+// Acquire at system scope on every XCD (workgroup w runs on XCD w % 8):
+// invalidates the L2 lines a peer's stores may have made stale, before the
+// owner reads what the peers wrote into its buffer.
+__global__ __launch_bounds__(64) void k_system_acquire() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 }
 
 // --------------------------------------------- 16-bit digit counts (P > 1)
@@ -1523,6 +1527,11 @@ hipError_t launch_peer_exchange(const Elem* src, int64_t m, int shift, int nbuck
   else
     hipLaunchKernelGGL(k_peer_scatter<false>, grid, dim3(kPlaceBlock), 0, s, src, m, shift, mask,
                        base, per, P, d);
+  return hipGetLastError();
+}
+
+hipError_t launch_system_acquire(hipStream_t s) {
+  hipLaunchKernelGGL(k_system_acquire, dim3(64), dim3(64), 0, s);
   return hipGetLastError();
 }
 

@@ -129,6 +129,8 @@ struct lsb_ctx {
   bool peer = false;          // exchange by direct stores into the owners' buffers
   bool peer_ready = false;    // peer tables set up
   bool onesweep = true;       // P == 1: single-read passes (k_subhist + k_onesweep)
+  bool self_coll = false;     // the self segment also goes through the collective
+  int64_t coll_calls = 0, coll_bytes = 0, coll_max = 0;  // element payload handed to the collective
   // What the last lsb_sort ran (lsb_get_last_sort).
   int last_local_passes = 0;
   int last_exchanges = 0;
@@ -460,14 +462,24 @@ int place_range(lsb_ctx* c, Rank& r, int shift, int src_rank, const Elem* src, i
   return LSB_OK;
 }
 
+// The receive buffer, allocated at the first all-to-all of the context.
+int ensure_recv(lsb_ctx* c, Rank& r) {
+  if (r.R) return LSB_OK;
+  HIP_TRY(hipSetDevice(r.dev));
+  return dev_alloc(&r.R, (size_t)c->per);
+}
+
 // The self segment needs no transfer: place it straight out of A as soon as
-// the plan is on the device (call after the host has the plan).
+// the plan is on the device (call after the host has the plan).  With
+// LSB_OPT_EXCHANGE_SELF it travels through the collective instead and is
+// placed from R by place_slice like every other source.
 int place_self(lsb_ctx* c, Rank& r, int shift) {
   const int me = r.rank;
   if (r.send_counts[me] != r.recv_counts[me])
     return fail(LSB_ERR_STATE, "exchange", "self count mismatch");
+  LSB_TRY(ensure_recv(c, r));
+  if (c->self_coll && c->mode != Mode::kLoopback) return LSB_OK;
   HIP_TRY(hipSetDevice(r.dev));
-  if (!r.R) LSB_TRY(dev_alloc(&r.R, (size_t)c->per));  // first all-to-all of this context
   HIP_TRY(hipEventRecord(r.pevent, r.stream));  // plan kernels done
   HIP_TRY(hipStreamWaitEvent(r.pstream, r.pevent, 0));
   return place_range(c, r, shift, me, r.A + r.send_displs[me], r.recv_displs[me],
@@ -480,8 +492,9 @@ int place_slice(lsb_ctx* c, Rank& r, int shift, int j) {
   HIP_TRY(hipSetDevice(r.dev));
   HIP_TRY(hipEventRecord(r.pevent, r.stream));
   HIP_TRY(hipStreamWaitEvent(r.pstream, r.pevent, 0));
+  const bool self_in_r = c->self_coll && c->mode != Mode::kLoopback;
   for (int s = 0; s < c->P; ++s) {
-    if (s == r.rank) continue;
+    if (s == r.rank && !self_in_r) continue;
     const int64_t lo = part(r.recv_counts[s], j, slices_of(c));
     const int64_t hi = part(r.recv_counts[s], j + 1, slices_of(c));
     LSB_TRY(place_range(c, r, shift, s, r.R + r.recv_displs[s] + lo, r.recv_displs[s] + lo, hi - lo));
@@ -571,6 +584,11 @@ int coll_allgather_u64(lsb_ctx* c, Rank& r, const uint64_t* send, uint64_t* recv
 int coll_alltoallv_u64(lsb_ctx* c, Rank& r, const uint64_t* send, const size_t* sc,
                        const size_t* sd, uint64_t* recv, const size_t* rc, const size_t* rd) {
   const int P = c->P;
+  int64_t call_bytes = 0;
+  for (int q = 0; q < P; ++q) call_bytes += (int64_t)sc[q] * 8;
+  c->coll_calls += 1;
+  c->coll_bytes += call_bytes;
+  c->coll_max = std::max(c->coll_max, call_bytes);
   if (c->mode == Mode::kRccl) {
     if (!c->p2p) {
       RCCL_TRY(ncclAllToAllv(send, sc, sd, recv, rc, rd, ncclUint64, c->comm, r.stream));
@@ -619,9 +637,11 @@ int coll_alltoallv_u64(lsb_ctx* c, Rank& r, const uint64_t* send, const size_t* 
 // placement pass.  Ordering: the counts all-gather cannot complete before
 // every rank's local pass has (stream order), so no store lands in a buffer
 // still being read; a barrier after the stores orders them before any
-// rank's next pass.  Visibility across GPUs relies on kernel boundaries
-// writing back / invalidating L2 (required on MI300-class parts even within
-// one device, whose XCDs have separate L2s).
+// rank's next pass.  Visibility across GPUs is made explicit rather than left
+// to kernel boundaries: k_peer_scatter ends every workgroup with a
+// system-scope release (L2 write-back of the XCD), and after the barrier the
+// owner runs a system-scope acquire on every XCD (L2 invalidate) before its
+// next pass reads the buffer.
 
 // Every rank's two physical buffers as this process sees them.
 int peer_setup(lsb_ctx* c) {
@@ -740,7 +760,12 @@ int exchange_peer(lsb_ctx* c, int digit) {
                                       r.stream));
   }
   LSB_TRY(peer_barrier(c));
-  for (Rank& r : c->ranks) std::swap(r.A, r.B);
+  for (Rank& r : c->ranks) {
+    // Acquire what the peers released (k_peer_scatter's system-scope fence).
+    HIP_TRY(hipSetDevice(r.dev));
+    HIP_TRY(lsb::launch_system_acquire(r.stream));
+    std::swap(r.A, r.B);
+  }
   return LSB_OK;
 }
 
@@ -764,7 +789,9 @@ int exchange_rccl(lsb_ctx* c, int digit) {
   const int me = r.rank;
   // ncclAllToAllv per slice (the reference's MPI_Alltoallv,
   // mpi/mpi_lsbsort.cpp:316-324), in uint64 units; the self entry is 0
-  // because the self segment was placed straight out of A.
+  // because the self segment was placed straight out of A (unless
+  // LSB_OPT_EXCHANGE_SELF sends it through the collective too).
+  const bool skip_self = !c->self_coll;
   std::vector<size_t> sc(P), sd(P), rc(P), rdp(P);
   for (int j = 0; j < slices_of(c); ++j) {
     {
@@ -774,8 +801,8 @@ int exchange_rccl(lsb_ctx* c, int digit) {
         const int64_t shi = part(r.send_counts[q], j + 1, slices_of(c));
         const int64_t rlo = part(r.recv_counts[q], j, slices_of(c));
         const int64_t rhi = part(r.recv_counts[q], j + 1, slices_of(c));
-        sc[q] = q == me ? 0 : (size_t)(shi - slo) * 2;
-        rc[q] = q == me ? 0 : (size_t)(rhi - rlo) * 2;
+        sc[q] = q == me && skip_self ? 0 : (size_t)(shi - slo) * 2;
+        rc[q] = q == me && skip_self ? 0 : (size_t)(rhi - rlo) * 2;
         sd[q] = (size_t)(r.send_displs[q] + slo) * 2;
         rdp[q] = (size_t)(r.recv_displs[q] + rlo) * 2;
       }
@@ -872,18 +899,9 @@ int sort_onesweep_rank(lsb_ctx* c, Rank& r, int* passes, uint64_t* varying) {
                              r.stream));
       r.os_epoch = 1;
     }
-#ifdef LSB_OS_NONEXT  // experiment: every pass's histogram from its own read
-    if (i > 0) {
-      Timer t(c, &r, LSB_K_UPSWEEP);
-      HIP_TRY(lsb::launch_subhist(r.A, m, shift, r.os_grid, hist[i & 1], nullptr, r.stream));
-    }
-    const int next_used = -1;
-#else
-    const int next_used = next;
-#endif
     {
       Timer t(c, &r, LSB_K_SCATTER);
-      HIP_TRY(lsb::launch_onesweep(r.A, r.B, m, shift, next_used, hist[i & 1], hist[(i + 1) & 1],
+      HIP_TRY(lsb::launch_onesweep(r.A, r.B, m, shift, next, hist[i & 1], hist[(i + 1) & 1],
                                    r.os_status, r.os_ctr, r.os_epoch,
                                    r.os_ctr + lsb::kOnesweepSubs, r.os_grid, r.stream));
       if (c->timing) c->scatter_elems += m;
@@ -1120,7 +1138,8 @@ int merge_slice(lsb_ctx* c, Rank& r, const MergeGeom& g, int j, Elem* F) {
   std::vector<Run> runs;
   for (int s = 0; s < c->P; ++s) {
     if (sr[s].len == 0) continue;
-    const Elem* p = s == r.rank ? r.A + r.mcut[s * K1 + (size_t)r.rank * g.S + j] : r.R + sr[s].roff;
+    const bool own = s == r.rank && !(c->self_coll && c->mode != Mode::kLoopback);
+    const Elem* p = own ? r.A + r.mcut[s * K1 + (size_t)r.rank * g.S + j] : r.R + sr[s].roff;
     runs.push_back({p, sr[s].len});
   }
   Timer t(c, &r, LSB_K_PLACE, r.pstream);
@@ -1235,9 +1254,10 @@ int exchange_merge(lsb_ctx* c) {
       std::vector<size_t> sc(P), sd(P), rc(P), rdp(P);
       for (int q = 0; q < P; ++q) {
         const size_t kq = (size_t)q * g.S + j;
-        sc[q] = q == r.rank ? 0 : (size_t)(r.mcut[(size_t)r.rank * K1 + kq + 1] - r.mcut[(size_t)r.rank * K1 + kq]) * 2;
+        const bool skip = q == r.rank && !c->self_coll;  // own range stays in A
+        sc[q] = skip ? 0 : (size_t)(r.mcut[(size_t)r.rank * K1 + kq + 1] - r.mcut[(size_t)r.rank * K1 + kq]) * 2;
         sd[q] = (size_t)r.mcut[(size_t)r.rank * K1 + kq] * 2;
-        rc[q] = q == r.rank ? 0 : (size_t)sr[q].len * 2;
+        rc[q] = skip ? 0 : (size_t)sr[q].len * 2;
         rdp[q] = (size_t)sr[q].roff * 2;
       }
       {
@@ -1541,6 +1561,9 @@ int lsb_set_option(lsb_ctx_t* c, int option, int64_t value) {
     case LSB_OPT_EXCHANGE_P2P:
       c->p2p = value != 0;
       return LSB_OK;
+    case LSB_OPT_EXCHANGE_SELF:
+      c->self_coll = value != 0;
+      return LSB_OK;
     case LSB_OPT_EXCHANGE_SLICES:
       if (value < 1 || value > 64)
         return fail(LSB_ERR_INVALID, "lsb_set_option", "exchange slices must be 1..64");
@@ -1765,6 +1788,22 @@ int lsb_get_scatter_elems(lsb_ctx_t* c, int64_t* elems) {
   if (elems) *elems = c->scatter_elems;
   return LSB_OK;
 }
+
+int lsb_get_exchange_bytes(lsb_ctx_t* c, int64_t* calls, int64_t* bytes, int64_t* max_call_bytes) {
+  LSB_TRY(check_ctx(c));
+  if (calls) *calls = c->coll_calls;
+  if (bytes) *bytes = c->coll_bytes;
+  if (max_call_bytes) *max_call_bytes = c->coll_max;
+  return LSB_OK;
+}
+
+#ifndef LSB_SOURCE_DIGEST
+#define LSB_SOURCE_DIGEST "unknown"
+#endif
+#ifndef LSB_BUILD_HOST
+#define LSB_BUILD_HOST "unknown"
+#endif
+const char* lsb_build_info(void) { return "sha256=" LSB_SOURCE_DIGEST " host=" LSB_BUILD_HOST; }
 
 // Host planner: see include/lsb.h.  For rank `me`, the global destination of
 // its j-th bucket-b record is gstart[b][me] + j with

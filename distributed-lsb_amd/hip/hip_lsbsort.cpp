@@ -14,9 +14,13 @@
 //              (default 0), exchange by device copies; same results as
 //              `mpirun -n P mpi_lsbsort` on one GPU.
 //   --json     also print one machine-readable line.
-//   --radix-bits 8|16|64  exchange digit width (local passes are always 8-bit);
-//              64: local sort, one all-to-all, merge of the P runs (the default
-//              with --gpus P > 1, as in bench.py; 8 otherwise)
+//   --radix-bits 8|16|64  exchange digit width (local passes are always 8-bit):
+//              16 (the reference's RADIX, one RCCL all-to-all per 16-bit digit;
+//              the default with --gpus P > 1, as in bench.py), 8 (8 all-to-alls;
+//              the default otherwise), or 64: local sort, ONE all-to-all, merge
+//              of the P runs
+//   --test-corrupt I  test hook: overwrite sorted record I before verifying
+//              (the failure report: every mismatch, Expected/Got, status 134)
 //   --dist uniform|zipf [--zipf-s S]   key distribution of the same pcg64 stream
 //   --exchange alltoallv|p2p|peer  element exchange (default RCCL AllToAllv in
 //              slices; grouped Send/Recv; direct peer stores, the shmem_putmem form)
@@ -24,6 +28,7 @@
 #include <sys/wait.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cinttypes>
 #include <cstdio>
@@ -50,6 +55,7 @@ struct Options {
   double zipf_s = 1.1;
   int exchange_option = -1;  // --exchange: LSB_OPT_EXCHANGE_P2P / _PEER, or -1 (AllToAllv)
   int slices = 0;            // --slices S (0: library default)
+  int64_t test_corrupt = -1; // --test-corrupt I: overwrite sorted record I (tests the report)
 };
 
 void flush_output() {
@@ -77,6 +83,7 @@ struct World {
   int nlocal = 1;
   int64_t n = 0;
   int64_t per = 0;
+  int dev = 0;  // device of this process's ranks
   bool root() const { return first == 0; }
   bool is_local(int r) const { return r >= first && r < first + nlocal; }
 };
@@ -105,6 +112,43 @@ void print_array(World& w, const char* name, int64_t n_per_rank) {
     }
     CHECK(lsb_barrier(w.ctx));
   }
+}
+
+// The reference's failure report (mpi/mpi_lsbsort.cpp:722-737): every
+// index whose record differs from std::stable_sort of the input by key,
+// with the expected and the actual record.  The input is regenerated on
+// this process's device (a loopback context of the same n, P and key
+// distribution: the same on-device PCG stream the sort started from), then
+// stable-sorted here; ranks print in rank order.
+void report_mismatches(World& w, const Options& o) {
+  lsb_ctx_t* gen = nullptr;
+  std::vector<int> devs(w.P, w.dev);
+  CHECK(lsb_create(&gen, o.n, w.P, devs.data(), 8));
+  CHECK(lsb_generate_ex(gen, o.dist, o.zipf_s));
+  std::vector<lsb_elem_t> expect((size_t)o.n);
+  for (int r = 0; r < w.P; ++r)
+    CHECK(lsb_copy_out(gen, r, 0, lsb_here(o.n, w.P, r), expect.data() + (size_t)r * w.per));
+  lsb_destroy(gen);
+  std::stable_sort(expect.begin(), expect.end(),
+                   [](const lsb_elem_t& a, const lsb_elem_t& b) { return a.key < b.key; });
+  std::vector<lsb_elem_t> got;
+  for (int r = 0; r < w.P; ++r) {
+    CHECK(lsb_barrier(w.ctx));
+    if (!w.is_local(r)) continue;
+    const int64_t here = lsb_here(o.n, w.P, r);
+    got.resize((size_t)here);
+    CHECK(lsb_copy_out(w.ctx, r, 0, here, got.data()));
+    for (int64_t i = 0; i < here; ++i) {
+      const lsb_elem_t& e = expect[(size_t)(r * w.per + i)];
+      const lsb_elem_t& g = got[(size_t)i];
+      if (e.key == g.key && e.val == g.val) continue;
+      printf("Sorted element %" PRId64 " did not match\n", r * w.per + i);
+      printf("Expected: (%016" PRIx64 ",%" PRIu64 ")\n", e.key, e.val);
+      printf("Got:      (%016" PRIx64 ",%" PRIu64 ")\n", g.key, g.val);
+    }
+    flush_output();
+  }
+  CHECK(lsb_barrier(w.ctx));
 }
 
 int run(World& w, const Options& o) {
@@ -152,6 +196,15 @@ int run(World& w, const Options& o) {
     CHECK(lsb_barrier(w.ctx));
   }
   if (o.print) print_array(w, "A", 10);
+  if (o.test_corrupt >= 0 && o.test_corrupt < o.n) {
+    // Test hook: overwrite one sorted record so the failure report can be checked.
+    const int r = (int)(o.test_corrupt / w.per);
+    if (w.is_local(r)) {
+      lsb_elem_t bad = {0x0123456789abcdefull, (uint64_t)o.n + 7};
+      CHECK(lsb_copy_in(w.ctx, r, o.test_corrupt - r * w.per, 1, &bad));
+    }
+    CHECK(lsb_barrier(w.ctx));
+  }
 
   int status = 0;
   if (o.verify) {
@@ -162,7 +215,6 @@ int run(World& w, const Options& o) {
     int64_t first_bad = -1;
     const int rc = lsb_verify(w.ctx, &first_bad);
     if (rc == LSB_ERR_VERIFY) {
-      if (w.root()) printf("Sorted element %" PRId64 " did not match\n", first_bad);
       status = 1;
     } else if (rc != LSB_OK) {
       die("lsb_verify", rc);
@@ -172,6 +224,15 @@ int run(World& w, const Options& o) {
     if (w.root()) printf(sorted ? "Array is sorted\n" : "Array is NOT sorted\n");
     if (!sorted) status = 1;
     flush_output();
+    if (status) {
+      // The reference then fails `assert(!failures)` (:737): exit with the
+      // status such an abort gives (134) after a clean teardown.
+      report_mismatches(w, o);
+      if (w.root()) fprintf(stderr, "hip_lsbsort: Assertion `!failures' failed.\n");
+      fflush(stderr);
+      lsb_destroy(w.ctx);
+      _exit(134);
+    }
   }
   if (o.json && w.root()) {
     printf("{\"n\": %" PRId64 ", \"ranks\": %d, \"sort_s\": %.9g, \"melem_per_s\": %.6g, "
@@ -202,6 +263,7 @@ int run_rank_process(const Options& o, int rank, int read_fd, const std::vector<
   w.per = lsb_per_rank(o.n, o.gpus);
   w.first = rank;
   w.nlocal = 1;
+  w.dev = rank;
   CHECK(lsb_create_rank(&w.ctx, o.n, o.gpus, rank, rank, o.radix_bits, id));
   const int status = run(w, o);
   lsb_destroy(w.ctx);
@@ -232,6 +294,7 @@ int main(int argc, char* argv[]) {
     else if (a == "--radix-bits") o.radix_bits = std::stoi(next());
     else if (a == "--zipf-s") o.zipf_s = std::stod(next());
     else if (a == "--slices") o.slices = std::stoi(next());
+    else if (a == "--test-corrupt") o.test_corrupt = std::stoll(next());
     else if (a == "--exchange") {
       const std::string x = next();
       if (x == "alltoallv") o.exchange_option = -1;
@@ -247,7 +310,7 @@ int main(int argc, char* argv[]) {
     }
   }
   if (!o.verify_set) o.verify = (o.n < 128LL * 1024 * 1024);
-  if (o.radix_bits == 0) o.radix_bits = o.gpus > 1 ? 64 : 8;
+  if (o.radix_bits == 0) o.radix_bits = o.gpus > 1 ? 16 : 8;
   if (o.n < 0 || o.ranks < 1 || o.gpus < 0) {
     fprintf(stderr, "invalid arguments\n");
     return 2;
@@ -286,9 +349,12 @@ int main(int argc, char* argv[]) {
     int worst = 0;
     for (pid_t pid : kids) {
       int st = 0;
-      if (waitpid(pid, &st, 0) < 0) worst = 2;
-      else if (WIFEXITED(st)) worst = WEXITSTATUS(st) > worst ? WEXITSTATUS(st) : worst;
-      else worst = 2;
+      int code = 2;
+      if (waitpid(pid, &st, 0) >= 0) {
+        if (WIFEXITED(st)) code = WEXITSTATUS(st);
+        else if (WIFSIGNALED(st)) code = 128 + WTERMSIG(st);  // e.g. 134: a rank's assert
+      }
+      worst = code > worst ? code : worst;
     }
     return worst;
   }
@@ -299,6 +365,7 @@ int main(int argc, char* argv[]) {
   w.per = lsb_per_rank(o.n, o.ranks);
   w.first = 0;
   w.nlocal = o.ranks;
+  w.dev = o.device;
   std::vector<int> devs(o.ranks, o.device);
   CHECK(lsb_create(&w.ctx, o.n, o.ranks, devs.data(), o.radix_bits));
   const int status = run(w, o);

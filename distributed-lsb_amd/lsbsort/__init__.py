@@ -48,6 +48,7 @@ KERNEL_NAMES = ("upsweep", "scan", "scatter", "exchange", "place", "sort")
 OPT_TIMING, OPT_FORCE_EXCHANGE, OPT_SKIP_CONSTANT_DIGITS, OPT_EXCHANGE_SLICES, OPT_EXCHANGE_P2P = 0, 1, 2, 3, 4
 OPT_EXCHANGE_PEER = 5
 OPT_ONESWEEP = 6
+OPT_EXCHANGE_SELF = 7
 
 
 class LsbError(RuntimeError):
@@ -153,6 +154,8 @@ def _lib() -> ctypes.CDLL:
             "lsb_get_kernel_stats": (i32, [vp, i32, P64, ctypes.POINTER(ctypes.c_double)]),
             "lsb_reset_kernel_stats": (i32, [vp]),
             "lsb_get_scatter_elems": (i32, [vp, P64]),
+            "lsb_get_exchange_bytes": (i32, [vp, P64, P64, P64]),
+            "lsb_build_info": (cp, []),
             "lsb_plan_exchange": (i32, [i64, i32, i32, i32, vp, vp, vp, vp, vp, vp]),
             "lsb_plan_exchange_device": (i32, [i32, i64, i32, i32, i32, vp, vp, vp, vp, vp, vp]),
             "lsb_plan_merge": (i32, [i64, i32, i32, vp, vp, vp, vp, vp, vp]),
@@ -177,6 +180,25 @@ def per_rank(n: int, P: int) -> int:
 
 def here(n: int, P: int, r: int) -> int:
     return int(_lib().lsb_here(n, P, r))
+
+
+def build_info() -> dict:
+    """{"sha256": digest of the sources the loaded library was built from,
+    "host": build host} (lsb_build_info)."""
+    info = _lib().lsb_build_info().decode()
+    return dict(kv.split("=", 1) for kv in info.split())
+
+
+def source_digest() -> str:
+    """sha256 of the library's sources as they are in this tree, in the
+    order the Makefile hashes them (SOURCES)."""
+    import hashlib
+    h = hashlib.sha256()
+    for rel in ("csrc/lsb_kernels.hip", "csrc/lsb_merge.hip", "csrc/lsb_runtime.cpp",
+                "csrc/lsb_kernels.h", "../include/lsb.h"):
+        with open(os.path.join(ROOT_DIR, rel), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
 
 
 def get_unique_id() -> bytes:
@@ -420,6 +442,13 @@ class World:
         e = ctypes.c_int64()
         _check(_lib().lsb_get_scatter_elems(self._h, ctypes.byref(e)), "lsb_get_scatter_elems")
         return int(e.value)
+
+    def exchange_bytes(self) -> tuple:
+        """(calls, bytes, largest call's bytes) handed to the all-to-all collective."""
+        c, b, mx = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        _check(_lib().lsb_get_exchange_bytes(self._h, ctypes.byref(c), ctypes.byref(b), ctypes.byref(mx)),
+               "lsb_get_exchange_bytes")
+        return int(c.value), int(b.value), int(mx.value)
 
 
 def mySort(world: World) -> None:  # noqa: N802 - reference name

@@ -86,6 +86,13 @@ typedef struct lsb_ctx lsb_ctx_t;
                                       offsets by decoupled look-back, histograms carried
                                       from pass to pass; 0: reduce-then-scan (count, scan,
                                       scatter) like every other pass */
+#define LSB_OPT_EXCHANGE_SELF   7  /* one-rank-per-process contexts: 1 sends the rank's own
+                                      segment through the element collective as well
+                                      (ncclAllToAllv / ncclSend+ncclRecv to itself, or the
+                                      caller's alltoallv) and places it from the receive
+                                      buffer like every other source; 0 (default) places it
+                                      straight out of A.  Same output; lets a world of one
+                                      carry the whole payload through RCCL (tests). */
 
 /* ---- geometry: DistributedArray::create (mpi/mpi_lsbsort.cpp:144-149) ---- */
 int64_t lsb_per_rank(int64_t n_total, int num_ranks);            /* ceil(n/P) */
@@ -196,6 +203,17 @@ int  lsb_get_kernel_stats(lsb_ctx_t* ctx, int kernel_id, int64_t* launches, doub
 int  lsb_reset_kernel_stats(lsb_ctx_t* ctx);
 /* Elements one launch of the scatter kernel processed, summed like the stats. */
 int  lsb_get_scatter_elems(lsb_ctx_t* ctx, int64_t* elems);
+/* Element payload this context handed to its all-to-all collective
+ * (ncclAllToAllv, grouped ncclSend/ncclRecv or the caller's alltoallv) since
+ * the context was created: calls, bytes sent (self segment included when
+ * LSB_OPT_EXCHANGE_SELF is on) and the largest one call sent.  Loopback
+ * contexts (device copies) report 0. */
+int  lsb_get_exchange_bytes(lsb_ctx_t* ctx, int64_t* calls, int64_t* bytes, int64_t* max_call_bytes);
+
+/* ---- build --------------------------------------------------------------- */
+/* "sha256=<digest of the sources the library was built from> host=<build
+ * host>" (static string).  tests/ compare the digest with the tree. */
+const char* lsb_build_info(void);
 
 /* ---- host planner (pure host code; used by the runtime when P > 1) ------- */
 /* Given hist[s*nbuckets + b] = number of elements of bucket b that rank s

@@ -41,6 +41,12 @@ def test_partition_helpers(lsb_built, oracle_mod):
                 assert lsb_built.here(n, P, r) == oracle_mod.here(n, P, r)
 
 
+def test_library_built_from_this_tree(lsb_built):
+    """The compiled-in source digest (lsb_build_info) equals the tree's."""
+    info = lsb_built.build_info()
+    assert info["sha256"] == lsb_built.source_digest(), info
+
+
 def test_strerror(lsb_built):
     lib = lsb_built._lib()
     assert lib.lsb_strerror(0) == b"ok"

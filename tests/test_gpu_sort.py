@@ -551,3 +551,23 @@ def test_zipf_verify_uses_zipf_keys(lsb_built):
         w.generate()  # uniform again: verify must recompute uniform keys
         w.my_sort()
         assert w.verify() == (True, -1)
+
+
+@pytest.mark.parametrize("mode", [["--ranks", "3"], ["--gpus", "1"]])
+def test_harness_reports_every_mismatch(lsb_built, oracle_mod, mode):
+    """A failed verify prints every bad index with Expected/Got, as the
+    reference does (mpi/mpi_lsbsort.cpp:729-737), and exits like its failed
+    assert (134)."""
+    n, bad = 5000, 1234
+    exe = lsb_built.HARNESS_PATH
+    r = subprocess.run([exe, "--n", str(n), "--verify", "--test-corrupt", str(bad)] + mode,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 134, (r.returncode, r.stderr)
+    P = int(mode[1])
+    expect = oracle_mod.stable_sort(oracle_mod.generate(n, P))[bad]
+    lines = r.stdout.splitlines()
+    i = lines.index(f"Sorted element {bad} did not match")
+    assert lines[i + 1] == f"Expected: ({int(expect['key']):016x},{int(expect['val'])})"
+    assert lines[i + 2] == f"Got:      (0123456789abcdef,{n + 7})"
+    assert sum(l.startswith("Sorted element ") for l in lines) == 1
+    assert "Array is NOT sorted" in lines or "Array is sorted" in lines
