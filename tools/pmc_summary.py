@@ -4,7 +4,6 @@
 Reads gpurun_out/prof/{stats,fetch,write}/ (rocprofv3 CSV) and writes
   profiles/<tag>_kernel_stats.csv   rocprofv3 --stats summary (copied)
   profiles/<tag>_pmc.json           per-kernel avg duration and HBM bytes per launch
-  profiles/pmc_scatter.json         what bench.py reports as roofline.traffic
 
 HBM bytes per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024, following
 MI355X_MICROARCH.md §HBM: on gfx950 FETCH_SIZE (KB) reads exactly half of a
@@ -68,14 +67,6 @@ def main(tag, prof=os.path.join(ROOT, "gpurun_out", "prof"),
            "kernels": kernels}
     with open(os.path.join(out_dir, f"{tag}_pmc.json"), "w") as f:
         json.dump(doc, f, indent=1)
-    sc = next((v for k, v in kernels.items() if k.startswith("k_scatter") or k.startswith("k_onesweep")), None)
-    if sc:
-        with open(os.path.join(out_dir, "pmc_scatter.json"), "w") as f:
-            json.dump({"tag": tag, "workload": workload,
-                       "kernel": next(k for k in kernels if kernels[k] is sc),
-                       "hbm_bytes_per_launch": sc["hbm_bytes_per_launch"],
-                       "algorithmic_bytes_per_launch": 32 * elems,
-                       "avg_ms": sc.get("avg_ms")}, f, indent=1)
     print(json.dumps(doc, indent=1))
 
 
