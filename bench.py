@@ -80,7 +80,7 @@ def parse():
                          "ncclSend/ncclRecv, or direct peer stores into the owners' buffers")
     ap.add_argument("--zipf-s", type=float, default=1.1)
     ap.add_argument("--passes", choices=("onesweep", "reduce-scan"), default="onesweep",
-                    help="N = 1 pass form: single-read (look-back) or count + scan + scatter")
+                    help="local pass form: single-read (look-back) or count + scan + scatter")
     return ap.parse_args()
 
 
@@ -422,9 +422,10 @@ def main():
         raise SystemExit("--exchange peer is a per-digit exchange form; use --radix-bits 8 or 16")
     w, device = make_world(a, d, N, n_total, radix)
     bind_device(device)
-    # Dominant kernel: the local pass.  Single-read passes run wherever a rank
-    # sorts its block alone: P = 1, and every rank of the whole-key exchange.
-    kernel = "k_onesweep" if ((N == 1 or radix == 64) and a.passes == "onesweep") else "k_scatter"
+    # Dominant kernel: the local pass.  Single-read passes (k_onesweep) in
+    # every form: P = 1, the per-digit exchange (the exchange's placement
+    # counts the next pass's histogram) and each rank of the whole-key form.
+    kernel = "k_onesweep" if a.passes == "onesweep" else "k_scatter"
 
     total, verified = timed_sorts(w, d, a, a.steps, a.warmup)
     stats = w.kernel_stats()
@@ -492,7 +493,9 @@ def main():
                  f"synthetic: zipf(s={a.zipf_s}) keys drawn from the pcg64(rank) stream (build-defined, SURVEY 8d C4)"),
         "config": {"workload": workload, "n_total": n_total, "n_per_gpu": a.n_per_gpu,
                    "local_digit_bits": 8, "local_passes": last[0], "exchanges": last[1],
-                   "pass_form": ("single-read (k_subhist once, k_onesweep per pass)" if kernel == "k_onesweep"
+                   "pass_form": (("single-read (k_subhist once, k_onesweep per pass" +
+                                  ("; k_place counts the next pass's histogram)" if N > 1 and radix != 64
+                                   else ")")) if kernel == "k_onesweep"
                                  else "reduce-then-scan (k_upsweep, k_scan, k_scatter per pass)"),
                    "exchange_digit_bits": radix if N > 1 else None,
                    "record_bytes": 16, "dist": a.dist,

@@ -99,17 +99,29 @@ hipError_t launch_subhist(const Elem* A, int64_t m, int shift, int grid, uint32_
 // (dequeue, load + rank, look-back + scan, stage, write, unused) over all
 // workgroups' thread 0; hipErrorNotSupported otherwise.
 hipError_t onesweep_profile(unsigned long long* out6, bool reset);
+// What a pass also hands the exchange that follows it (per-digit exchange
+// forms, P > 1): totals[b] = the pass's 256 digit counts; count16 (zeroed
+// here) = the 65536 counts of the 16-bit digit at shift - 8, for the high
+// byte of a 16-bit exchange digit whose input is sorted by the low byte.
+struct OnesweepExtra {
+  uint64_t* totals = nullptr;
+  uint64_t* count16 = nullptr;
+};
 hipError_t launch_onesweep(const Elem* in, Elem* out, int64_t m, int shift, int next_shift,
                            const uint32_t* sub_hist, uint32_t* next_hist, uint64_t* status,
                            uint32_t* tile_ctr, uint32_t epoch, uint32_t* err, int grid,
-                           hipStream_t s);
+                           hipStream_t s, OnesweepExtra extra = OnesweepExtra());
 
 // Receiver-side placement of one source's received range: src[i] (receive
 // index k0 + i) goes to out[off_row[digit] + k0 + i], off_row = the source's
 // row of the placement table (place_off[s * nbuckets ...]); out holds
 // out_len records (the receive order [k0, k0 + count) lies inside it).
+// next_shift >= 0: also add the placed records' digit at next_shift to
+// next_hist[x * 256 + b] (x = the out position's onesweep sub-array over
+// out_len records; zeroed by the caller): the next local pass's sub_hist.
 hipError_t launch_place(const Elem* src, Elem* out, int64_t out_len, int64_t k0, int64_t count,
-                        int shift, int nbuckets, const int64_t* off_row, hipStream_t s);
+                        int shift, int nbuckets, const int64_t* off_row, hipStream_t s,
+                        int next_shift = -1, uint32_t* next_hist = nullptr);
 
 // Peer-store exchange (opt-in, LSB_OPT_EXCHANGE_PEER): from the all-gathered
 // counts hist[s * nb + b], rank `me` writes each of its m bucket-ordered

@@ -92,14 +92,16 @@ __device__ __forceinline__ uint32_t mbcnt(uint64_t mask) {
 // sign-extended (0 or ~0), bal = lanes with the bit set, and the lanes whose
 // bit equals mine are ~(bal ^ t); one gfx950 v_bitop3 per 32-bit half folds
 // that into the running mask (truth table 0x90 = a & ~(b ^ c), index
-// a*4 + b*2 + c).  4 VALU per bit; the select form (set ? bal : ~bal)
-// compiles to 9.
+// a*4 + b*2 + c).  4 VALU per bit: v_bfe_i32, v_cmp_ne (the ballot, taken
+// on t itself through the compare intrinsic; __ballot(t != 0) let the
+// compiler re-derive the bit with a shift, 5 per bit), two v_bitop3.  The
+// select form (set ? bal : ~bal) compiles to 9.
 __device__ __forceinline__ uint64_t match_digit8(uint32_t d, uint64_t active) {
   uint32_t lo = (uint32_t)active, hi = (uint32_t)(active >> 32);
 #pragma unroll
   for (int bit = 0; bit < 8; ++bit) {
     const uint32_t t = (uint32_t)__builtin_amdgcn_sbfe((int)d, bit, 1);
-    const uint64_t bal = __ballot(t != 0u);
+    const uint64_t bal = __builtin_amdgcn_uicmp(t, 0u, 33);  // ICMP_NE: lanes whose bit is set
     lo = __builtin_amdgcn_bitop3_b32(lo, (uint32_t)bal, t, 0x90);
     hi = __builtin_amdgcn_bitop3_b32(hi, (uint32_t)(bal >> 32), t, 0x90);
   }
@@ -712,12 +714,24 @@ __device__ unsigned long long g_os_prof[8];
 #define OS_MARK(k) ((void)0)
 #endif
 
-template <int BLOCK, int IPT, bool NEXT>
+//
+// For the per-digit exchange forms (P > 1) a pass also hands the exchange its
+// counts: `totals` (workgroup 0 writes the 256 digit totals), and with C16
+// (the high byte of a 16-bit exchange digit) the 65536 counts of the 16-bit
+// digit at shift16 = shift - 8.  The input is then sorted by that low byte,
+// so a tile whose first and last records share it has one low byte
+// throughout, and its bucket-b run adds cnt_b to count16[b][lo]; thread b
+// keeps a running count per (b, lo) in registers and adds it to memory when
+// its tile's low byte changes (a workgroup's tiles are taken in order, so
+// that is a few times per launch).  A tile across a low-byte boundary walks
+// its staged runs.
+template <int BLOCK, int IPT, bool NEXT, bool C16>
 __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
     const Elem* __restrict__ in, Elem* __restrict__ out, int64_t m, int shift, int next_shift,
     const uint32_t* __restrict__ sub_hist, uint32_t* __restrict__ next_hist,
     unsigned long long* __restrict__ status, uint32_t* __restrict__ tile_ctr, uint32_t epoch,
-    uint32_t* __restrict__ err) {
+    uint32_t* __restrict__ err, uint64_t* __restrict__ totals,
+    unsigned long long* __restrict__ count16) {
   constexpr int W = BLOCK / 64;
   constexpr int T = BLOCK * IPT;
   static_assert(BLOCK == kBuckets, "one thread per bucket in the look-back");
@@ -730,12 +744,20 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
   __shared__ uint64_t scan64[W];
   __shared__ uint32_t scan32[W];
   __shared__ int32_t s_tile, s_sub;
+  __shared__ uint32_t tile_lo[2];  // C16: low byte of the tile's first, last record
 
   const int t = threadIdx.x;
   const int w = t >> 6;
   const uint32_t lane = lane_id();
   const int64_t TT = (m + T - 1) / T;
   const uint32_t tag_agg = 2u * epoch, tag_pre = 2u * epoch + 1u;
+  const int shift16 = shift - 8;
+  uint32_t acc_lo = 0xFFFFFFFFu;  // C16: thread t's running count of digit (t, acc_lo)
+  uint64_t acc = 0;
+  auto c16_flush = [&]() {
+    if (acc) atomicAdd(count16 + (((uint32_t)t << 8) | acc_lo), (unsigned long long)acc);
+    acc = 0;
+  };
 
   // Bucket starts (exclusive scan of the digit totals) and this thread's
   // bucket column of the sub-array histogram.
@@ -748,11 +770,12 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
   }
   uint64_t all;
   const uint64_t bstart = block_exclusive_scan<BLOCK>(tot, scan64, &all);
+  if (totals != nullptr && blockIdx.x == 0) totals[t] = tot;
   // Skewed digit (one bucket holds more than 1/32 of the records, e.g. Zipf
   // keys): runs of equal next digits are then long, and 64 lanes adding to
-  // one LDS counter serialise.  Such launches add once per wave-instruction
-  // whose records share a slot; uniform keys keep the plain add (the check
-  // costs them 5.7 %, tools/ab.sh).  Launch-uniform.
+  // one LDS counter serialise.  Such launches add once per run of equal
+  // slots within a wave-instruction; uniform keys keep the plain add (a
+  // per-instruction check costs them 5.7 %, tools/ab.sh).  Launch-uniform.
   const bool skewed = NEXT && __syncthreads_or(tot > (uint64_t)(m >> 5)) != 0;
   if (NEXT)
     for (int i = t; i < kSub * kBuckets; i += BLOCK) nh[i] = 0;
@@ -847,6 +870,11 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
       const uint32_t pre = wcnt[w][d];
       rk[i] = pre + below;
       if (valid && below == 0) wcnt[w][d] = pre + (uint32_t)__popcll(mt);
+      if (C16) {
+        const int li = wbase + i * 64;
+        if (li == 0) tile_lo[0] = (uint32_t)(e[i].key >> shift16) & 0xFFu;
+        if (li == nvalid - 1) tile_lo[1] = (uint32_t)(e[i].key >> shift16) & 0xFFu;
+      }
     }
     __syncthreads();
     OS_MARK(1);  // load + rank
@@ -855,6 +883,18 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
       const uint32_t v = wcnt[ww][t];
       wcnt[ww][t] = cnt;
       cnt += v;
+    }
+    bool mixed16 = false;
+    if (C16) {
+      const uint32_t l0 = tile_lo[0];
+      mixed16 = l0 != tile_lo[1];
+      if (!mixed16 && cnt > 0) {
+        if (l0 != acc_lo) {
+          c16_flush();
+          acc_lo = l0;
+        }
+        acc += cnt;
+      }
     }
     const uint32_t cnt_b = pair_swap(cnt);  // even lanes: lane t + 1's count
     if (even) {
@@ -946,13 +986,20 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
           const uint32_t dn = (uint32_t)(v.key >> next_shift) & (kBuckets - 1);
           const uint32_t slot = xs * kBuckets + dn;
           if (kSkew) {
-            // One add per wave-instruction whose records share the slot.
-            const uint32_t s0 = __builtin_amdgcn_readfirstlane(slot);
+            // One add per run of equal slots within the wave-instruction: the
+            // head lane of each run adds the run's length.  Hot keys come in
+            // long runs in the staged (bucket-ordered) tile, so the 64-way
+            // same-address LDS atomics that serialise become one or two adds.
+            // Active lanes are a prefix (j < nvalid), so a run ends at the
+            // next head or at the active count.
             const uint64_t act = __ballot(1);
-            if (__ballot(slot == s0) == act) {
-              if (mbcnt(act) == 0) atomicAdd(&nh[s0], (uint32_t)__popcll(act));
-            } else {
-              atomicAdd(&nh[slot], 1u);
+            const uint32_t prev = (uint32_t)__shfl_up((int)slot, 1, 64);
+            const bool head = lane == 0 || prev != slot;
+            const uint64_t heads = __ballot(head);
+            if (head) {
+              const uint64_t above = heads & ~((2ull << lane) - 1ull);
+              const uint32_t end = above ? (uint32_t)__builtin_ctzll(above) : (uint32_t)__popcll(act);
+              atomicAdd(&nh[slot], end - lane);
             }
           } else {
             atomicAdd(&nh[slot], 1u);
@@ -962,9 +1009,20 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
     };
     if (skewed) write_out(std::true_type{});
     else write_out(std::false_type{});
+    if (C16 && mixed16) {  // the tile crosses a low-byte boundary: walk run t
+      for (uint32_t k = 0; k < cnt; ++k) {
+        const uint32_t l = (uint32_t)(stage[lstart + k].key >> shift16) & 0xFFu;
+        if (l != acc_lo) {
+          c16_flush();
+          acc_lo = l;
+        }
+        ++acc;
+      }
+    }
     __syncthreads();
     OS_MARK(4);  // write
   }
+  if (C16) c16_flush();
 #ifdef LSB_OS_PROFILE
   if (t == 0)
     for (int k = 0; k < 6; ++k) atomicAdd(&g_os_prof[k], (unsigned long long)prof[k]);
@@ -979,25 +1037,38 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
 constexpr int kPlaceBlock = 256;
 constexpr int kPlaceIpt = 8;
 constexpr int kPlaceLdsBuckets = 4096;  // offset rows up to here (32 KiB) are staged in LDS
+constexpr int kPlaceNextGrid = 1024;    // k_place<., kNext> grid cap (one flush per workgroup)
 
 // One source's received range: record k in [k0, k0 + count) of the receive
 // order (src[k - k0]) goes to out[off[digit] + k], off = that source's row of
 // the placement table.  The exchange launches it per source and per slice,
 // so a slice is placed while the next one is still in flight.
-template <bool kLds>
+//
+// kNext (per-digit exchange with single-read local passes): the placement
+// also counts the next local digit (at next_shift) of every record by the
+// onesweep sub-array of its output position over out_len records, in LDS,
+// added to next_hist at the end: the next pass's sub_hist, so that pass
+// needs no count read (k_subhist).  The exchange launches one k_place per
+// (source, slice); they all add into one next_hist.
+template <bool kLds, bool kNext>
 __global__ __launch_bounds__(kPlaceBlock) void k_place(const Elem* __restrict__ src,
                                                        Elem* __restrict__ out, int64_t k0,
                                                        int64_t count, int shift, uint32_t mask,
                                                        const int64_t* __restrict__ off_row,
-                                                       int64_t out_len) {
+                                                       int64_t out_len, int next_shift,
+                                                       uint32_t* __restrict__ next_hist) {
   __shared__ int64_t lds_off[kLds ? kPlaceLdsBuckets : 1];
+  __shared__ uint32_t nh[kNext ? kSub * kBuckets : 1];
   const int nb = (int)mask + 1;
   const int64_t* off = off_row;
+  const int64_t TT = (out_len + kTile - 1) / kTile;
+  if (kNext)
+    for (int i = threadIdx.x; i < kSub * kBuckets; i += kPlaceBlock) nh[i] = 0;
   if (kLds) {
     for (int i = threadIdx.x; i < nb; i += kPlaceBlock) lds_off[i] = off_row[i];
-    __syncthreads();
     off = lds_off;
   }
+  if (kLds || kNext) __syncthreads();
   // kPlaceIpt records in flight per thread (a 1-record grid-stride loop
   // reached 4.4 TB/s; streaming copies need several loads outstanding).
   const int64_t step = (int64_t)gridDim.x * kPlaceBlock * kPlaceIpt;
@@ -1014,10 +1085,20 @@ __global__ __launch_bounds__(kPlaceBlock) void k_place(const Elem* __restrict__ 
       const int64_t k = base + (int64_t)i * kPlaceBlock;
       if (k < count) {
         const uint32_t d = (uint32_t)(x[i].key >> shift) & mask;
-        LSB_DASSERT(off[d] + k0 + k >= 0 && off[d] + k0 + k < out_len);
-        store_elem(out + (off[d] + k0 + k), x[i]);
+        const int64_t g = off[d] + k0 + k;
+        LSB_DASSERT(g >= 0 && g < out_len);
+        store_elem(out + g, x[i]);
+        if (kNext) {
+          const uint32_t xs = (uint32_t)sub_of_tile(g / kTile, TT);
+          atomicAdd(&nh[xs * kBuckets + ((uint32_t)(x[i].key >> next_shift) & (kBuckets - 1))], 1u);
+        }
       }
     }
+  }
+  if (kNext) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < kSub * kBuckets; i += kPlaceBlock)
+      if (nh[i]) atomicAdd(&next_hist[i], nh[i]);
   }
 }
 
@@ -1468,7 +1549,7 @@ hipError_t launch_subhist(const Elem* A, int64_t m, int shift, int grid, uint32_
 hipError_t launch_onesweep(const Elem* in, Elem* out, int64_t m, int shift, int next_shift,
                            const uint32_t* sub_hist, uint32_t* next_hist, uint64_t* status,
                            uint32_t* tile_ctr, uint32_t epoch, uint32_t* err, int grid,
-                           hipStream_t s) {
+                           hipStream_t s, OnesweepExtra extra) {
   if (m <= 0) return hipSuccess;
   if (m > kOnesweepMaxElems || epoch == 0 || epoch >= (1u << 31) || shift < 0 || shift > 56 ||
       next_shift > 56)
@@ -1480,33 +1561,57 @@ hipError_t launch_onesweep(const Elem* in, Elem* out, int64_t m, int shift, int 
   int64_t g = grid < kSub ? kSub : grid;
   if (g > (TT + kSub - 1) / kSub * kSub) g = (TT + kSub - 1) / kSub * kSub;
   auto* st = reinterpret_cast<unsigned long long*>(status);
-  if (next_shift >= 0) {
+  auto* c16 = reinterpret_cast<unsigned long long*>(extra.count16);
+  if (c16) {
+    // The 16-bit counts need the low byte below this digit, and no next
+    // digit: the exchange follows this pass.
+    if (shift < 8 || next_shift >= 0) return hipErrorInvalidValue;
+    e = hipMemsetAsync(c16, 0, sizeof(uint64_t) * 65536, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((k_onesweep<kScatterBlock, kScatterIpt, false, true>), dim3((unsigned)g),
+                       dim3(kScatterBlock), 0, s, in, out, m, shift, 0, sub_hist, nullptr, st,
+                       tile_ctr, epoch, err, extra.totals, c16);
+  } else if (next_shift >= 0) {
     e = hipMemsetAsync(next_hist, 0, sizeof(uint32_t) * kSub * kBuckets, s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_onesweep<kScatterBlock, kScatterIpt, true>), dim3((unsigned)g),
+    hipLaunchKernelGGL((k_onesweep<kScatterBlock, kScatterIpt, true, false>), dim3((unsigned)g),
                        dim3(kScatterBlock), 0, s, in, out, m, shift, next_shift, sub_hist,
-                       next_hist, st, tile_ctr, epoch, err);
+                       next_hist, st, tile_ctr, epoch, err, extra.totals, nullptr);
   } else {
-    hipLaunchKernelGGL((k_onesweep<kScatterBlock, kScatterIpt, false>), dim3((unsigned)g),
+    hipLaunchKernelGGL((k_onesweep<kScatterBlock, kScatterIpt, false, false>), dim3((unsigned)g),
                        dim3(kScatterBlock), 0, s, in, out, m, shift, 0, sub_hist, nullptr, st,
-                       tile_ctr, epoch, err);
+                       tile_ctr, epoch, err, extra.totals, nullptr);
   }
   return hipGetLastError();
 }
 
 hipError_t launch_place(const Elem* src, Elem* out, int64_t out_len, int64_t k0, int64_t count,
-                        int shift, int nbuckets, const int64_t* off_row, hipStream_t s) {
+                        int shift, int nbuckets, const int64_t* off_row, hipStream_t s,
+                        int next_shift, uint32_t* next_hist) {
   if (count <= 0) return hipSuccess;
   if (nbuckets != 256 && nbuckets != 65536) return hipErrorInvalidValue;
   if (k0 < 0 || k0 + count > out_len) return hipErrorInvalidValue;
-  const dim3 grid(grid_for(count, kPlaceBlock * kPlaceIpt, 4096));
   const uint32_t mask = (uint32_t)nbuckets - 1;
-  if (nbuckets <= kPlaceLdsBuckets)
-    hipLaunchKernelGGL(k_place<true>, grid, dim3(kPlaceBlock), 0, s, src, out, k0, count, shift,
-                       mask, off_row, out_len);
+  const bool lds = nbuckets <= kPlaceLdsBuckets;
+  if (next_shift >= 0) {
+    if (next_shift > 56 || !next_hist || out_len > kOnesweepMaxElems) return hipErrorInvalidValue;
+    // Fewer, longer-lived workgroups: each flushes its 8 x 256 counters once.
+    const dim3 grid(grid_for(count, kPlaceBlock * kPlaceIpt, kPlaceNextGrid));
+    if (lds)
+      hipLaunchKernelGGL((k_place<true, true>), grid, dim3(kPlaceBlock), 0, s, src, out, k0, count,
+                         shift, mask, off_row, out_len, next_shift, next_hist);
+    else
+      hipLaunchKernelGGL((k_place<false, true>), grid, dim3(kPlaceBlock), 0, s, src, out, k0, count,
+                         shift, mask, off_row, out_len, next_shift, next_hist);
+    return hipGetLastError();
+  }
+  const dim3 grid(grid_for(count, kPlaceBlock * kPlaceIpt, 4096));
+  if (lds)
+    hipLaunchKernelGGL((k_place<true, false>), grid, dim3(kPlaceBlock), 0, s, src, out, k0, count,
+                       shift, mask, off_row, out_len, 0, nullptr);
   else
-    hipLaunchKernelGGL(k_place<false>, grid, dim3(kPlaceBlock), 0, s, src, out, k0, count, shift,
-                       mask, off_row, out_len);
+    hipLaunchKernelGGL((k_place<false, false>), grid, dim3(kPlaceBlock), 0, s, src, out, k0, count,
+                       shift, mask, off_row, out_len, 0, nullptr);
   return hipGetLastError();
 }
 

@@ -94,6 +94,15 @@ struct Rank {
   uint32_t* os_err_h = nullptr;         // pinned mirror of the error word
   uint32_t os_epoch = 0;                // last look-back epoch
   int os_grid = 0;                      // persistent grid (2 workgroups per CU)
+  // Per-digit exchange with single-read local passes (sort_exchange_onesweep):
+  // os_hist[os_cur] is A's sub-array histogram of the byte at os_valid (-1:
+  // none; the next pass reads A once with k_subhist).  The exchange's
+  // placements count the byte at place_next into place_hist as they write.
+  int os_cur = 0;
+  int os_valid = -1;
+  int place_next = -1;
+  uint32_t* place_hist = nullptr;
+  bool counts_ready = false;            // totals16 = this exchange digit's counts (k_onesweep C16)
   // Whole-key exchange (radix_bits = 64), allocated on first use.
   uint64_t* split_state = nullptr;      // [Q][2] key interval per target
   int64_t* split_targets = nullptr;     // [Q] global positions q * per
@@ -394,6 +403,10 @@ int digit_counts(lsb_ctx* c, Rank& r, int digit, const uint64_t** counts) {
     *counts = r.totals;  // k_scan totals of the (only) sub-pass
     return LSB_OK;
   }
+  if (r.counts_ready) {  // counted by the high-byte k_onesweep
+    *counts = r.totals16;
+    return LSB_OK;
+  }
   HIP_TRY(hipSetDevice(r.dev));
   {
     Timer t(c, &r, LSB_K_UPSWEEP);
@@ -458,7 +471,8 @@ int place_range(lsb_ctx* c, Rank& r, int shift, int src_rank, const Elem* src, i
   if (cnt <= 0) return LSB_OK;
   Timer t(c, &r, LSB_K_PLACE, r.pstream);
   HIP_TRY(lsb::launch_place(src, r.B, r.here, k0, cnt, shift, c->nb,
-                            r.place + (size_t)src_rank * c->nb, r.pstream));
+                            r.place + (size_t)src_rank * c->nb, r.pstream, r.place_next,
+                            r.place_hist));
   return LSB_OK;
 }
 
@@ -822,6 +836,7 @@ int exchange_rccl(lsb_ctx* c, int digit) {
 // is the identity and is skipped (all ~0 = run everything).  want_span: the
 // first sub-pass also reduces the key span (lsb_sort, digit 0).
 int merge_sort(lsb_ctx* c);
+int exchange_digit(lsb_ctx* c, int digit);
 
 int do_pass(lsb_ctx* c, int digit, uint64_t varying = ~0ull, bool want_span = false) {
   if (c->bits == 64 && exchanging(c)) return merge_sort(c);  // the one 64-bit digit
@@ -837,6 +852,10 @@ int do_pass(lsb_ctx* c, int digit, uint64_t varying = ~0ull, bool want_span = fa
   }
   if (!exchanging(c)) return LSB_OK;
   ++c->last_exchanges;
+  return exchange_digit(c, digit);
+}
+
+int exchange_digit(lsb_ctx* c, int digit) {
   if (c->peer) return exchange_peer(c, digit);
   if (c->mode != Mode::kLoopback) return exchange_rccl(c, digit);
   return exchange_loopback(c, digit);
@@ -860,6 +879,17 @@ int onesweep_ensure(Rank& r) {
   HIP_TRY(hipMemsetAsync(r.os_ctr, 0, 2 * lsb::kOnesweepSubs * sizeof(uint32_t), r.stream));
   r.os_epoch = 0;
   r.os_grid = max_chunks_for_device(r.dev);
+  return LSB_OK;
+}
+
+// A fresh look-back epoch for the next k_onesweep launch of rank r.
+int next_epoch(Rank& r) {
+  if (++r.os_epoch >= (1u << 30)) {  // tags 2*epoch(+1) stay below 2^31; start over
+    HIP_TRY(hipMemsetAsync(r.os_status, 0,
+                           (size_t)lsb::onesweep_tiles(r.here) * lsb::kBuckets * sizeof(uint64_t),
+                           r.stream));
+    r.os_epoch = 1;
+  }
   return LSB_OK;
 }
 
@@ -893,12 +923,7 @@ int sort_onesweep_rank(lsb_ctx* c, Rank& r, int* passes, uint64_t* varying) {
   for (size_t i = 0; i < digits.size(); ++i) {
     const int shift = digits[i] * lsb::kDigitBits;
     const int next = i + 1 < digits.size() ? digits[i + 1] * lsb::kDigitBits : -1;
-    if (++r.os_epoch >= (1u << 30)) {  // tags 2*epoch(+1) stay below 2^31; start over
-      HIP_TRY(hipMemsetAsync(r.os_status, 0,
-                             (size_t)lsb::onesweep_tiles(m) * lsb::kBuckets * sizeof(uint64_t),
-                             r.stream));
-      r.os_epoch = 1;
-    }
+    LSB_TRY(next_epoch(r));
     {
       Timer t(c, &r, LSB_K_SCATTER);
       HIP_TRY(lsb::launch_onesweep(r.A, r.B, m, shift, next, hist[i & 1], hist[(i + 1) & 1],
@@ -917,6 +942,150 @@ int sort_onesweep_rank(lsb_ctx* c, Rank& r, int* passes, uint64_t* varying) {
 
 int sort_onesweep(lsb_ctx* c) {
   return sort_onesweep_rank(c, c->ranks[0], &c->last_local_passes, &c->last_varying);
+}
+
+// ---- per-digit exchange with single-read local passes ----------------------
+// lsb_sort of the per-digit exchange forms (radix_bits 8 / 16, P > 1): the
+// reference's pass loop (mpi/mpi_lsbsort.cpp:580-585), each exchange digit's
+// localShuffle (:213-247) as one or two k_onesweep passes instead of count +
+// scan + scatter.  One k_subhist read per sort gives the first byte's
+// sub-array histogram and the key span; after that every histogram is
+// counted by whatever writes the records: the previous local pass, or the
+// exchange's k_place launches (their output is the next pass's input).  The
+// last local pass of an exchange digit hands the exchange its counts: the
+// 256 totals, or (16-bit digits) the 65536 counts, from the high-byte pass.
+bool exchange_onesweep_applies(const lsb_ctx* c) {
+  if (!c->onesweep || !exchanging(c) || c->bits == 64) return false;
+  for (const Rank& r : c->ranks)
+    if (r.here > lsb::kOnesweepMaxElems) return false;
+  return true;
+}
+
+// One local pass of rank r on the byte at `shift`; next >= 0: also count the
+// byte at `next` over the output (the next local pass follows directly).
+int local_pass_os(lsb_ctx* c, Rank& r, int shift, int next, lsb::OnesweepExtra extra) {
+  HIP_TRY(hipSetDevice(r.dev));
+  r.starts_fused = false;
+  const int64_t m = r.here;
+  if (m == 0) {
+    if (extra.totals) HIP_TRY(hipMemsetAsync(extra.totals, 0, sizeof(uint64_t) * lsb::kBuckets, r.stream));
+    if (extra.count16) HIP_TRY(hipMemsetAsync(extra.count16, 0, sizeof(uint64_t) * 65536, r.stream));
+    r.os_valid = -1;
+    return LSB_OK;
+  }
+  uint32_t* hist[2] = {r.os_hist, r.os_hist + lsb::kOnesweepSubs * lsb::kBuckets};
+  if (r.os_valid != shift) {  // nothing counted this byte over A: read it
+    Timer t(c, &r, LSB_K_UPSWEEP);
+    HIP_TRY(lsb::launch_subhist(r.A, m, shift, r.os_grid, hist[r.os_cur], nullptr, r.stream));
+  }
+  LSB_TRY(next_epoch(r));
+  {
+    Timer t(c, &r, LSB_K_SCATTER);
+    HIP_TRY(lsb::launch_onesweep(r.A, r.B, m, shift, next, hist[r.os_cur], hist[r.os_cur ^ 1],
+                                 r.os_status, r.os_ctr, r.os_epoch, r.os_ctr + lsb::kOnesweepSubs,
+                                 r.os_grid, r.stream, extra));
+    if (c->timing) c->scatter_elems += m;
+  }
+  std::swap(r.A, r.B);
+  if (next >= 0) {
+    r.os_cur ^= 1;
+    r.os_valid = next;
+  } else {
+    r.os_valid = -1;
+  }
+  return LSB_OK;
+}
+
+int gather_span(lsb_ctx* c, uint64_t* kor, uint64_t* knor);
+
+int sort_exchange_onesweep(lsb_ctx* c) {
+  const int D = 64 / c->bits, subs = c->bits / lsb::kDigitBits;
+  for (Rank& r : c->ranks) {
+    HIP_TRY(hipSetDevice(r.dev));
+    LSB_TRY(onesweep_ensure(r));
+    HIP_TRY(hipMemsetAsync(r.span, 0, 2 * sizeof(uint64_t), r.stream));
+    r.os_cur = 0;
+    r.os_valid = -1;
+    if (r.here > 0) {
+      Timer t(c, &r, LSB_K_UPSWEEP);
+      HIP_TRY(lsb::launch_subhist(r.A, r.here, 0, r.os_grid, r.os_hist,
+                                  c->skip_constant ? r.span : nullptr, r.stream));
+      r.os_valid = 0;
+    }
+  }
+  uint64_t varying = ~0ull;
+  if (c->skip_constant) {
+    uint64_t kor = 0, knor = 0;
+    LSB_TRY(gather_span(c, &kor, &knor));
+    varying = kor & knor;
+  }
+  c->last_varying = varying;
+  // Local passes in order; an exchange follows the last one of each digit.
+  // A digit on which every key agrees needs neither (its stable pass and its
+  // (digit, rank) exchange order are the identity), nor does a constant byte
+  // its local pass.
+  struct Step {
+    int shift, digit;
+    bool exch;
+  };
+  std::vector<Step> steps;
+  const uint64_t dmask = (1ull << c->bits) - 1;
+  for (int d = 0; d < D; ++d) {
+    if (((varying >> (d * c->bits)) & dmask) == 0) continue;
+    for (int sub = 0; sub < subs; ++sub) {
+      const int shift = d * c->bits + sub * lsb::kDigitBits;
+      if (((varying >> shift) & (lsb::kBuckets - 1)) != 0) steps.push_back({shift, d, false});
+    }
+    steps.back().exch = true;
+  }
+  for (size_t i = 0; i < steps.size(); ++i) {
+    const Step& st = steps[i];
+    const int after = i + 1 < steps.size() ? steps[i + 1].shift : -1;
+    // 16-bit digit: its high-byte pass counts the 65536 digits (a constant
+    // high byte leaves the count to digit_counts' read of A).
+    const bool c16 = c->bits == 16 && st.exch && st.shift == st.digit * 16 + lsb::kDigitBits;
+    for (Rank& r : c->ranks) {
+      lsb::OnesweepExtra x;
+      if (st.exch && c->bits == 8) x.totals = r.totals;
+      if (c16) x.count16 = r.totals16;
+      r.counts_ready = c16;
+      LSB_TRY(local_pass_os(c, r, st.shift, st.exch ? -1 : after, x));
+    }
+    ++c->last_local_passes;
+    if (!st.exch) continue;
+    for (Rank& r : c->ranks) {
+      r.place_next = c->peer || r.here == 0 ? -1 : after;
+      r.place_hist = nullptr;
+      if (r.place_next >= 0) {
+        r.place_hist = r.os_hist + (size_t)(r.os_cur ^ 1) * lsb::kOnesweepSubs * lsb::kBuckets;
+        HIP_TRY(hipSetDevice(r.dev));
+        HIP_TRY(hipMemsetAsync(r.place_hist, 0, sizeof(uint32_t) * lsb::kOnesweepSubs * lsb::kBuckets,
+                               r.stream));
+      }
+    }
+    ++c->last_exchanges;
+    const int rc = exchange_digit(c, st.digit);
+    for (Rank& r : c->ranks) {
+      if (rc == LSB_OK && r.place_next >= 0) {
+        r.os_cur ^= 1;
+        r.os_valid = r.place_next;
+      } else {
+        r.os_valid = -1;
+      }
+      r.place_next = -1;
+      r.place_hist = nullptr;
+      r.counts_ready = false;
+    }
+    LSB_TRY(rc);
+  }
+  // The look-back's give-up word, read by lsb_sync.
+  for (Rank& r : c->ranks) {
+    if (r.here == 0) continue;
+    HIP_TRY(hipSetDevice(r.dev));
+    HIP_TRY(hipMemcpyAsync(r.os_err_h, r.os_ctr + lsb::kOnesweepSubs, sizeof(uint32_t),
+                           hipMemcpyDeviceToHost, r.stream));
+  }
+  return LSB_OK;
 }
 
 // ---- whole-key exchange (radix_bits = 64) ----------------------------------
@@ -1648,6 +1817,8 @@ int lsb_sort(lsb_ctx_t* c) {
     LSB_TRY(merge_sort(c));
   } else if (onesweep_applies(c)) {
     LSB_TRY(sort_onesweep(c));
+  } else if (exchange_onesweep_applies(c)) {
+    LSB_TRY(sort_exchange_onesweep(c));
   } else if (!c->skip_constant) {
     for (int d = 0; d < passes; ++d) LSB_TRY(do_pass(c, d));
   } else {

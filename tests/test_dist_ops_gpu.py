@@ -96,7 +96,7 @@ def test_processes_peer_store_exchange(tmp_path, digests, oracle_mod, world, bit
 
 @pytest.mark.parametrize("world,bits,mask,passes,exchanges", [
     (2, 8, 0x00000000FFFFFFFF, 4, 4),
-    (3, 16, 0x00FF0000000000FF, 3, 2),   # digit 0; digit 3's low byte; digits 1, 2 skipped
+    (3, 16, 0x00FF0000000000FF, 2, 2),   # digits 0 and 3, each its low byte only; 1, 2 skipped
     (3, 64, 0x00FF0000000000FF, 2, 1),   # whole-key exchange: local passes on bytes 0 and 6
 ])
 def test_processes_skip_constant_digits(tmp_path, oracle_mod, world, bits, mask, passes, exchanges):

@@ -153,27 +153,33 @@ def _masked_keys(n, mask, rng):
     return a
 
 
-# (key mask, radix bits, P) -> 8-bit local passes and exchanges lsb_sort must run.
-# Digit 0 always runs (the key span comes out of its count kernel).
-@pytest.mark.parametrize("mask,bits,P,passes,exchanges", [
-    (0xFFFFFFFF, 8, 1, 4, 0),                 # keys < 2^32: bytes 4..7 constant
-    (0xFFFF0000000000FF, 8, 1, 3, 0),         # bytes 1..5 constant
-    (0xFFFFFFFFFFFFFFFF, 8, 1, 8, 0),         # nothing to skip
-    (0x0, 8, 1, 1, 0),                        # all keys 0: only the first pass
-    (0x0000000000FFFFFF, 8, 3, 3, 3),         # 3 digits, each with its exchange
-    (0x0000000000FFFFFF, 16, 3, 3, 2),        # 16-bit: digits 0,1; byte 3 skipped
-    (0xFF00000000000000, 16, 4, 3, 2),        # 16-bit: digit 0 always, digit 3 only its high byte
-    (0x00000000FFFF0000, 16, 8, 4, 2),        # digit 0 forced (constant), digit 1 runs
+# (key mask, radix bits, P) -> 8-bit local passes and exchanges lsb_sort must
+# run, with reduce-then-scan passes (digit 0 always runs: the key span comes
+# out of its count kernel) and with single-read passes (P = 1 runs digit 0
+# too; the per-digit exchange forms read the span with k_subhist before any
+# pass, so a constant digit 0 is skipped like any other).
+@pytest.mark.parametrize("mask,bits,P,passes,exchanges,passes_os,exchanges_os", [
+    (0xFFFFFFFF, 8, 1, 4, 0, 4, 0),                 # keys < 2^32: bytes 4..7 constant
+    (0xFFFF0000000000FF, 8, 1, 3, 0, 3, 0),         # bytes 1..5 constant
+    (0xFFFFFFFFFFFFFFFF, 8, 1, 8, 0, 8, 0),         # nothing to skip
+    (0x0, 8, 1, 1, 0, 1, 0),                        # all keys 0: only the first pass
+    (0x0000000000FFFFFF, 8, 3, 3, 3, 3, 3),         # 3 digits, each with its exchange
+    (0x0000000000FFFFFF, 16, 3, 3, 2, 3, 2),        # 16-bit: digits 0,1; byte 3 skipped
+    (0xFF00000000000000, 16, 4, 3, 2, 1, 1),        # 16-bit: digit 3's high byte (+ digit 0 forced)
+    (0x00000000FFFF0000, 16, 8, 4, 2, 2, 1),        # digit 1 (+ digit 0 forced)
 ])
-def test_constant_digits_skipped(lsb_built, oracle_mod, mask, bits, P, passes, exchanges):
+@pytest.mark.parametrize("onesweep", [1, 0])
+def test_constant_digits_skipped(lsb_built, oracle_mod, mask, bits, P, passes, exchanges,
+                                 passes_os, exchanges_os, onesweep):
     rng = np.random.default_rng(mask & 0xFFFF ^ P)
     a = _masked_keys(100_003, mask, rng)
     with lsb_built.World(a.size, ranks=P, radix_bits=bits) as w:
+        w.set_option(lsb_built.OPT_ONESWEEP, onesweep)
         w.scatter_global(a)
         w.my_sort()
         assert np.array_equal(w.gather_global(), oracle_mod.stable_sort(a))
         lp, ex, varying = w.last_sort()
-        assert (lp, ex) == (passes, exchanges)
+        assert (lp, ex) == ((passes_os, exchanges_os) if onesweep else (passes, exchanges))
         assert varying & ~mask == 0
 
 
@@ -198,7 +204,8 @@ def test_constant_digits_skipped_over_rccl(lsb_built, oracle_mod):
         w.my_sort()
         w.sync()
         assert np.array_equal(w.copy_out(0), oracle_mod.stable_sort(a))
-        assert w.last_sort()[:2] == (3, 2)  # digit 0 (both bytes), byte 2; digits 0 and 1
+        # byte 0 (digit 0's high byte is constant), byte 2; digits 0 and 1
+        assert w.last_sort()[:2] == (2, 2)
     finally:
         w.close()
 

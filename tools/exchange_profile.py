@@ -17,18 +17,22 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "distributed-lsb_amd"))
 import lsbsort  # noqa: E402
 
-CASES = [  # (n, P, bits, force_exchange)
-    (1 << 30, 1, 8, False),
-    (1 << 30, 1, 8, True),
-    (1 << 30, 1, 16, True),
-    (1 << 30, 2, 8, False),
-    (1 << 30, 2, 16, False),
-    (1 << 30, 4, 16, False),
+CASES = [  # (n, P, bits, force_exchange, single-read local passes)
+    (1 << 30, 1, 8, False, 1),
+    (1 << 30, 1, 8, True, 1),
+    (1 << 30, 1, 8, True, 0),
+    (1 << 30, 1, 16, True, 1),
+    (1 << 30, 1, 16, True, 0),
+    (1 << 30, 2, 16, False, 1),
+    (1 << 30, 2, 16, False, 0),
+    (1 << 30, 4, 16, False, 1),
+    (1 << 30, 4, 16, False, 0),
 ]
 
 
-def run(n, P, bits, force, steps=2):
+def run(n, P, bits, force, onesweep, steps=2):
     with lsbsort.World(n, ranks=P, radix_bits=bits) as w:
+        w.set_option(lsbsort.OPT_ONESWEEP, onesweep)
         if force:
             w.set_option(lsbsort.OPT_FORCE_EXCHANGE, 1)
         w.generate()
@@ -47,7 +51,8 @@ def run(n, P, bits, force, steps=2):
         st = w.kernel_stats()
         ok, _ = w.verify()
     per = {k: round(v[1] / steps, 3) for k, v in st.items() if v[0]}
-    return {"n": n, "P": P, "bits": bits, "force_exchange": force, "ms_per_sort": round(t / steps * 1e3, 2),
+    return {"n": n, "P": P, "bits": bits, "force_exchange": force, "onesweep": onesweep,
+            "ms_per_sort": round(t / steps * 1e3, 2),
             "melem_s": round(n / (t / steps) / 1e6, 1), "kernel_ms_per_sort": per, "verified": ok}
 
 
