@@ -85,14 +85,18 @@ hipError_t launch_starts_to_counts(const int64_t* first16, int64_t m, uint64_t* 
 // = tiles [x*TT/8, (x+1)*TT/8).  sub_hist[x * 256 + b] = count of digit b
 // in sub-array x.
 constexpr int kOnesweepSubs = 8;
-constexpr int64_t kOnesweepMaxElems = int64_t(1) << 34;  // 32-bit look-back values
+// Look-back values are 30 bits (a bucket's count within one sub-array of
+// m / 8 + kTile records): m < 2^33 - 2^16, i.e. 137 GB per record buffer.
+constexpr int64_t kOnesweepMaxElems = (int64_t(1) << 33) - (int64_t(1) << 16);
 inline int64_t onesweep_tiles(int64_t m) { return (m + kTile - 1) / kTile; }
 // sub_hist (zeroed here) of the digit at `shift`; span as for launch_upsweep.
 hipError_t launch_subhist(const Elem* A, int64_t m, int shift, int grid, uint32_t* sub_hist,
                           uint64_t* span, hipStream_t s);
 // One stable pass in -> out on the digit at `shift`, offsets from sub_hist
-// plus a look-back over status (onesweep_tiles(m) * 256 words, zeroed once at
-// allocation; epoch >= 1, new for every launch).  next_shift >= 0: also
+// plus a look-back over status (onesweep_tiles(m) * 256 u32 granules, zeroed
+// once at allocation; epoch >= 1, new for every launch over the same m, and
+// the first launch after a zeroing odd: a granule's tag is the epoch's
+// parity, so every launch must write every row).  next_shift >= 0: also
 // next_hist (zeroed here) = sub_hist of the digit at next_shift over out.
 // tile_ctr: kOnesweepSubs words of scratch; *err |= 1 if a look-back gave up.
 // -DLSB_OS_PROFILE builds: summed s_memtime ticks of k_onesweep's phases
@@ -108,7 +112,7 @@ struct OnesweepExtra {
   uint64_t* count16 = nullptr;
 };
 hipError_t launch_onesweep(const Elem* in, Elem* out, int64_t m, int shift, int next_shift,
-                           const uint32_t* sub_hist, uint32_t* next_hist, uint64_t* status,
+                           const uint32_t* sub_hist, uint32_t* next_hist, uint32_t* status,
                            uint32_t* tile_ctr, uint32_t epoch, uint32_t* err, int grid,
                            hipStream_t s, OnesweepExtra extra = OnesweepExtra());
 

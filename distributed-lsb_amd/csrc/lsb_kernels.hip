@@ -163,9 +163,6 @@ __device__ __forceinline__ uint32_t wave_inclusive_scan<uint32_t>(uint32_t v) {
 __device__ __forceinline__ uint32_t pair_swap(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, false);
 }
-__device__ __forceinline__ uint64_t pair_swap(uint64_t v) {
-  return ((uint64_t)pair_swap((uint32_t)(v >> 32)) << 32) | pair_swap((uint32_t)v);
-}
 
 // Exclusive scan over the whole workgroup (every thread must call it).
 // `tmp` needs BLOCK/64 entries.  *total receives the block sum.
@@ -571,14 +568,18 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_scatter(const Elem* __re
 //     excl[t][b] + rank in tile, where sub_pre = exclusive prefix of the
 //     sub-array histogram over x (known before the pass) and excl = the
 //     sum of b-counts of earlier tiles of the same sub-array, found by a
-//     look-back over status granules: status[t][b] = {value, tag} in one
-//     8-byte word, tag = 2*epoch + 1 for an inclusive prefix, 2*epoch for the
-//     tile's own count ("aggregate"), anything else = not yet published.
-//     Buckets b, b+1 travel as one 16-byte write-through (sc1) buffer store,
-//     polled with 16-byte sc1 loads (the guide's R2 form: the data is the
-//     flag, no fences); each half carries its own tag and a pair is used
-//     only when both agree.  The epoch is new every launch, so status needs
-//     no reset.  The tile publishes its aggregate right after ranking and
+//     look-back over status granules: status[t][b] = one self-tagged u32,
+//     bits 0-29 the value, bit 30 set for an inclusive prefix (clear: the
+//     tile's own count, its "aggregate"), bit 31 the launch's epoch parity.
+//     Every launch writes every tile's row (a context's m never changes), so
+//     a row holds either this launch's value or the previous launch's, whose
+//     parity differs: status needs no reset (zeroed once at allocation; the
+//     first launch has parity 1), and a granule is half the bytes of a
+//     {value, tag} word pair (the status traffic was 6 % of the pass's HBM
+//     bytes).  Buckets b, b+1 travel as one 8-byte write-through (sc1) buffer
+//     store, polled with 8-byte sc1 loads (the guide's R2 form: the data is
+//     the flag, no fences); each half carries its own tag and a pair is used
+//     only when both agree.  The tile publishes its aggregate right after ranking and
 //     reads its predecessor while it scans and stages; one predecessor per
 //     round trip measured fastest (wider windows: +6 % at 2, +11 % at 4),
 //     and the next tile's id is fetched while this one's records are written.
@@ -592,7 +593,7 @@ constexpr uint32_t kSpinLimit = 1u << 22;  // look-back polls before giving up (
 constexpr int kPollSleep = 1;              // s_sleep between look-back polls (4, 16: no change)
 
 typedef __attribute__((address_space(1))) uint32_t gu32;
-typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+typedef uint32_t v2u __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ int64_t sub_first_tile(int x, int64_t TT) { return (int64_t)x * TT / kSub; }
 // Sub-array of tile t = (8t + 7) / TT without a division: the number of
@@ -729,7 +730,7 @@ template <int BLOCK, int IPT, bool NEXT, bool C16>
 __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
     const Elem* __restrict__ in, Elem* __restrict__ out, int64_t m, int shift, int next_shift,
     const uint32_t* __restrict__ sub_hist, uint32_t* __restrict__ next_hist,
-    unsigned long long* __restrict__ status, uint32_t* __restrict__ tile_ctr, uint32_t epoch,
+    uint32_t* __restrict__ status, uint32_t* __restrict__ tile_ctr, uint32_t epoch,
     uint32_t* __restrict__ err, uint64_t* __restrict__ totals,
     unsigned long long* __restrict__ count16) {
   constexpr int W = BLOCK / 64;
@@ -750,7 +751,9 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
   const int w = t >> 6;
   const uint32_t lane = lane_id();
   const int64_t TT = (m + T - 1) / T;
-  const uint32_t tag_agg = 2u * epoch, tag_pre = 2u * epoch + 1u;
+  // Granule tags (bits 30-31): this launch's parity, and the prefix bit.
+  constexpr uint32_t kValMask = (1u << 30) - 1u, kPreBit = 1u << 30;
+  const uint32_t tag_agg = (epoch & 1u) << 31, tag_pre = tag_agg | kPreBit;
   const int shift16 = shift - 8;
   uint32_t acc_lo = 0xFFFFFFFFu;  // C16: thread t's running count of digit (t, acc_lo)
   uint64_t acc = 0;
@@ -843,18 +846,18 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
     }
     // Status rows of this sub-array through one buffer descriptor (byte
     // offsets < 2^31); the even lane of a pair publishes and polls buckets
-    // t, t + 1 as one 16-byte sc1 access: two self-tagged 8-byte halves,
+    // t, t + 1 as one 8-byte sc1 access: two self-tagged 4-byte halves,
     // written by one store, so a pair is consumed only when both tags agree.
     const int64_t first = sub_first_tile(x, TT);
     const int64_t last = sub_first_tile(x + 1, TT);
     const bool head = tile == first;
     const bool even = (lane & 1u) == 0;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        status + first * kBuckets, 0, (int)((last - first) * kBuckets * 8), 0x00020000);
-    constexpr uint32_t kRowBytes = kBuckets * 8;
-    const uint32_t my_off = (uint32_t)(tile - first) * kRowBytes + (uint32_t)t * 8u;
+        status + first * kBuckets, 0, (int)((last - first) * kBuckets * 4), 0x00020000);
+    constexpr uint32_t kRowBytes = kBuckets * 4;
+    const uint32_t my_off = (uint32_t)(tile - first) * kRowBytes + (uint32_t)t * 4u;
     uint32_t prow = (uint32_t)(tile - first) - 1u;  // newest predecessor row not yet summed
-    v4u g = {0u, 0u, 0u, 0u};
+    v2u g = {0u, 0u};
     uint32_t cnt = 0, lstart;
     // Stable rank of every element among the wave's elements of its digit
     // (per-wave counters), then the tile's counts: publish the aggregate,
@@ -899,8 +902,8 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
     const uint32_t cnt_b = pair_swap(cnt);  // even lanes: lane t + 1's count
     if (even) {
       const uint32_t tg = head ? tag_pre : tag_agg;
-      __builtin_amdgcn_raw_buffer_store_b128(v4u{cnt, tg, cnt_b, tg}, rs, my_off, 0, 16);
-      if (!head) g = __builtin_amdgcn_raw_buffer_load_b128(rs, prow * kRowBytes + (uint32_t)t * 8u, 0, 16);
+      __builtin_amdgcn_raw_buffer_store_b64(v2u{cnt | tg, cnt_b | tg}, rs, my_off, 0, 16);
+      if (!head) g = __builtin_amdgcn_raw_buffer_load_b64(rs, prow * kRowBytes + (uint32_t)t * 4u, 0, 16);
     }
     {
       uint32_t tile_total;
@@ -918,14 +921,15 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
       }
     }
 
-    uint64_t ea = 0, eb = 0;
+    uint32_t ea = 0, eb = 0;
     if (even && !head) {
       uint32_t spins = 0;
       for (;;) {
-        if (g.y == g.w && (g.y == tag_pre || g.y == tag_agg)) {
-          ea += g.x;
-          eb += g.z;
-          if (g.y == tag_pre) break;
+        // Both halves of this launch (parity) and of one kind (prefix bit).
+        if (((g.x ^ g.y) >> 30) == 0 && (g.x & ~kValMask & ~kPreBit) == tag_agg) {
+          ea += g.x & kValMask;
+          eb += g.y & kValMask;
+          if (g.x & kPreBit) break;
           --prow;
         } else {
           __builtin_amdgcn_s_sleep(kPollSleep);
@@ -936,12 +940,12 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
             break;
           }
         }
-        g = __builtin_amdgcn_raw_buffer_load_b128(rs, prow * kRowBytes + (uint32_t)t * 8u, 0, 16);
+        g = __builtin_amdgcn_raw_buffer_load_b64(rs, prow * kRowBytes + (uint32_t)t * 4u, 0, 16);
       }
-      __builtin_amdgcn_raw_buffer_store_b128(
-          v4u{(uint32_t)(ea + cnt), tag_pre, (uint32_t)(eb + cnt_b), tag_pre}, rs, my_off, 0, 16);
+      __builtin_amdgcn_raw_buffer_store_b64(v2u{(ea + cnt) | tag_pre, (eb + cnt_b) | tag_pre}, rs,
+                                            my_off, 0, 16);
     }
-    const uint64_t eb_left = pair_swap(eb);  // odd lanes: lane t - 1's sum
+    const uint32_t eb_left = pair_swap(eb);  // odd lanes: lane t - 1's sum
     const uint64_t excl = even ? ea : eb_left;
     const int64_t R = (int64_t)(base + excl);  // first output slot of the run
     delta[t] = R - (int64_t)lstart;
@@ -1547,7 +1551,7 @@ hipError_t launch_subhist(const Elem* A, int64_t m, int shift, int grid, uint32_
 }
 
 hipError_t launch_onesweep(const Elem* in, Elem* out, int64_t m, int shift, int next_shift,
-                           const uint32_t* sub_hist, uint32_t* next_hist, uint64_t* status,
+                           const uint32_t* sub_hist, uint32_t* next_hist, uint32_t* status,
                            uint32_t* tile_ctr, uint32_t epoch, uint32_t* err, int grid,
                            hipStream_t s, OnesweepExtra extra) {
   if (m <= 0) return hipSuccess;
@@ -1560,7 +1564,7 @@ hipError_t launch_onesweep(const Elem* in, Elem* out, int64_t m, int shift, int 
   // Persistent grid, a multiple of the XCD count; no more than the tiles.
   int64_t g = grid < kSub ? kSub : grid;
   if (g > (TT + kSub - 1) / kSub * kSub) g = (TT + kSub - 1) / kSub * kSub;
-  auto* st = reinterpret_cast<unsigned long long*>(status);
+  uint32_t* st = status;
   auto* c16 = reinterpret_cast<unsigned long long*>(extra.count16);
   if (c16) {
     // The 16-bit counts need the low byte below this digit, and no next

@@ -88,7 +88,7 @@ struct Rank {
   std::vector<void*> ipc_opened;
   int64_t* peer_base = nullptr;         // [nb]
   // Single-read passes (LSB_OPT_ONESWEEP, P == 1), allocated on first use.
-  uint64_t* os_status = nullptr;        // [tiles][256] look-back granules
+  uint32_t* os_status = nullptr;        // [tiles][256] look-back granules (self-tagged u32)
   uint32_t* os_hist = nullptr;          // [2][8][256] sub-array histograms (ping-pong)
   uint32_t* os_ctr = nullptr;           // [8] tile counters, [8] look-back error word
   uint32_t* os_err_h = nullptr;         // pinned mirror of the error word
@@ -875,7 +875,7 @@ int onesweep_ensure(Rank& r) {
   LSB_TRY(dev_alloc(&r.os_ctr, 2 * lsb::kOnesweepSubs));
   LSB_TRY(host_alloc(&r.os_err_h, 1));
   *r.os_err_h = 0;
-  HIP_TRY(hipMemsetAsync(r.os_status, 0, tiles * lsb::kBuckets * sizeof(uint64_t), r.stream));
+  HIP_TRY(hipMemsetAsync(r.os_status, 0, tiles * lsb::kBuckets * sizeof(uint32_t), r.stream));
   HIP_TRY(hipMemsetAsync(r.os_ctr, 0, 2 * lsb::kOnesweepSubs * sizeof(uint32_t), r.stream));
   r.os_epoch = 0;
   r.os_grid = max_chunks_for_device(r.dev);
@@ -883,13 +883,10 @@ int onesweep_ensure(Rank& r) {
 }
 
 // A fresh look-back epoch for the next k_onesweep launch of rank r.
+// Granules carry the epoch's parity, and every launch rewrites every row, so
+// only the alternation matters (the counter runs on for the record).
 int next_epoch(Rank& r) {
-  if (++r.os_epoch >= (1u << 30)) {  // tags 2*epoch(+1) stay below 2^31; start over
-    HIP_TRY(hipMemsetAsync(r.os_status, 0,
-                           (size_t)lsb::onesweep_tiles(r.here) * lsb::kBuckets * sizeof(uint64_t),
-                           r.stream));
-    r.os_epoch = 1;
-  }
+  if (++r.os_epoch >= (1u << 30)) r.os_epoch = 2;  // 2^30 is even: keep the alternation
   return LSB_OK;
 }
 
@@ -1483,6 +1480,10 @@ int onesweep_check(Rank& r) {
   if (!r.os_err_h || *r.os_err_h == 0) return LSB_OK;
   *r.os_err_h = 0;
   HIP_TRY(hipMemset(r.os_ctr + lsb::kOnesweepSubs, 0, sizeof(uint32_t)));
+  // A launch that gave up may have left rows of an older parity: start the
+  // granules over (zeroed; the next launch is odd).
+  HIP_TRY(hipMemset(r.os_status, 0, (size_t)lsb::onesweep_tiles(r.here) * lsb::kBuckets * sizeof(uint32_t)));
+  r.os_epoch = 0;
   return fail(LSB_ERR_HIP, "k_onesweep", "look-back timed out; output invalid");
 }
 

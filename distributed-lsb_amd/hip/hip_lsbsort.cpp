@@ -50,7 +50,7 @@ struct Options {
   int ranks = 1;
   int device = 0;
   bool json = false;
-  int radix_bits = 0;        // --radix-bits (0: 64 with --gpus > 1, else 8)
+  int radix_bits = 0;        // --radix-bits (0: 16 with --gpus > 1, else 8)
   int dist = LSB_DIST_UNIFORM;
   double zipf_s = 1.1;
   int exchange_option = -1;  // --exchange: LSB_OPT_EXCHANGE_P2P / _PEER, or -1 (AllToAllv)

@@ -81,11 +81,12 @@ typedef struct lsb_ctx lsb_ctx_t;
                                       (shmem_putmem / MPI_Put form; IPC-mapped across
                                       processes); no receive buffer, no placement pass.
                                       Opt-in: set on every rank before the first sort. */
-#define LSB_OPT_ONESWEEP        6  /* 1 (default): lsb_sort on a context that exchanges
-                                      nothing (P == 1) reads each record once per pass:
-                                      offsets by decoupled look-back, histograms carried
-                                      from pass to pass; 0: reduce-then-scan (count, scan,
-                                      scatter) like every other pass */
+#define LSB_OPT_ONESWEEP        6  /* 1 (default): lsb_sort reads each record once per
+                                      local pass (P == 1, the per-digit exchange forms and
+                                      the whole-key form's local sort): offsets by decoupled
+                                      look-back, histograms carried from pass to pass (or
+                                      counted by the exchange's placement); 0: reduce-then-
+                                      scan (count, scan, scatter), as lsb_pass always is */
 #define LSB_OPT_EXCHANGE_SELF   7  /* one-rank-per-process contexts: 1 sends the rank's own
                                       segment through the element collective as well
                                       (ncclAllToAllv / ncclSend+ncclRecv to itself, or the
