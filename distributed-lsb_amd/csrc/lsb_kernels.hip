@@ -996,9 +996,13 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
             // same-address LDS atomics that serialise become one or two adds.
             // Active lanes are a prefix (j < nvalid), so a run ends at the
             // next head or at the active count.
+            // The previous lane's slot by DPP wave_shr:1 (lane 0 keeps ~slot,
+            // so it is always a head); __shfl_up is a ds_bpermute round trip
+            // (-1.5 % Zipf, uniform unchanged: profiles/ab/r02_ab7_*).
             const uint64_t act = __ballot(1);
-            const uint32_t prev = (uint32_t)__shfl_up((int)slot, 1, 64);
-            const bool head = lane == 0 || prev != slot;
+            const uint32_t prev =
+                (uint32_t)__builtin_amdgcn_update_dpp((int)~slot, (int)slot, 0x138, 0xf, 0xf, false);
+            const bool head = prev != slot;
             const uint64_t heads = __ballot(head);
             if (head) {
               const uint64_t above = heads & ~((2ull << lane) - 1ull);

@@ -13,7 +13,11 @@ import lsbsort  # noqa: E402
 lg = int(sys.argv[1]) if len(sys.argv) > 1 else 30
 DIST = os.environ.get("LSB_DIST", "uniform")  # uniform | zipf
 n = 1 << lg
-w = lsbsort.World(n, 1)
+# LSB_RADIX_BITS=16 and LSB_FORCE_EXCHANGE=1: the per-digit exchange path at
+# P = 1 (counts, plan, k_place), as tools/exchange_profile.py, with LSB_DIST keys.
+w = lsbsort.World(n, 1, radix_bits=int(os.environ.get("LSB_RADIX_BITS", "8")))
+if os.environ.get("LSB_FORCE_EXCHANGE") == "1":
+    w.set_option(lsbsort.OPT_FORCE_EXCHANGE, 1)
 # LSB_PASSES=reduce-scan: count + scan + scatter per pass instead of single-read passes
 w.set_option(lsbsort.OPT_ONESWEEP, 0 if os.environ.get("LSB_PASSES") == "reduce-scan" else 1)
 w.set_timing(True)
