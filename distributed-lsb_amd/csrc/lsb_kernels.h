@@ -102,7 +102,7 @@ hipError_t launch_subhist(const Elem* A, int64_t m, int shift, int grid, uint32_
 // -DLSB_OS_PROFILE builds: summed s_memtime ticks of k_onesweep's phases
 // (dequeue, load + rank, look-back + scan, stage, write, unused) over all
 // workgroups' thread 0; hipErrorNotSupported otherwise.
-hipError_t onesweep_profile(unsigned long long* out6, bool reset);
+hipError_t onesweep_profile(unsigned long long* out10, bool reset);
 // What a pass also hands the exchange that follows it (per-digit exchange
 // forms, P > 1): totals[b] = the pass's 256 digit counts; count16 (zeroed
 // here) = the 65536 counts of the 16-bit digit at shift - 8, for the high

@@ -591,16 +591,25 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_scatter(const Elem* __re
 constexpr int kSub = kOnesweepSubs;
 constexpr uint32_t kSpinLimit = 1u << 22;  // look-back polls before giving up (seconds)
 constexpr int kPollSleep = 1;              // s_sleep between look-back polls (4, 16: no change)
+// Look-back rows in flight per round trip.  Wider windows lose: 2 / 4 / 8
+// rows +3.8 / +7.3 / +12.8 % per sort (profiles/ab/r02_ab8_uniform.log; a
+// tile then sums more rows, 6.7 instead of 5.0 at 4, as the extra loads
+// slow every poll).
+constexpr int kLookW = 1;
+// Status stores write through (sc1): plain stores stay dirty in the
+// writer's L2 and a poller never saw them (look-back timed out,
+// gpurun_out/ab10).
+constexpr int kStPol = 16;
 
 typedef __attribute__((address_space(1))) uint32_t gu32;
 typedef uint32_t v2u __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ int64_t sub_first_tile(int x, int64_t TT) { return (int64_t)x * TT / kSub; }
-// Sub-array of tile t = (8t + 7) / TT without a division: the number of
-// x in 1..7 with x * TT <= 8t + 7 (32-bit exact: TT < 2^22, see
-// kOnesweepMaxElems).
+// Sub-array of tile t without a division: the number of x in 1..kSub-1
+// with x * TT <= kSub * t + kSub - 1, i.e. floor(x * TT / kSub) <= t
+// (32-bit exact: TT < 2^22, see kOnesweepMaxElems).
 __device__ __forceinline__ int sub_of_tile(int64_t t, int64_t TT) {
-  const uint32_t num = 8u * (uint32_t)t + 7u, tt = (uint32_t)TT;
+  const uint32_t num = (uint32_t)kSub * (uint32_t)t + (uint32_t)(kSub - 1), tt = (uint32_t)TT;
   int x = 0;
 #pragma unroll
   for (int k = 1; k < kSub; ++k) x += num >= (uint32_t)k * tt ? 1 : 0;
@@ -702,7 +711,7 @@ __global__ __launch_bounds__(BLOCK) void k_subhist(const Elem* __restrict__ A, i
 // workgroup adds s_memtime deltas between the barriers of a tile into
 // g_os_prof[phase]; the runtime prints them at lsb_destroy.
 #ifdef LSB_OS_PROFILE
-__device__ unsigned long long g_os_prof[8];
+__device__ unsigned long long g_os_prof[10];
 #define OS_MARK(k)                                                       \
   do {                                                                   \
     if (t == 0) {                                                        \
@@ -784,7 +793,7 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
     for (int i = t; i < kSub * kBuckets; i += BLOCK) nh[i] = 0;
 
 #ifdef LSB_OS_PROFILE
-  uint64_t prof[6] = {0, 0, 0, 0, 0, 0};
+  uint64_t prof[10] = {};  // phases 0-6; 7: rows summed in look-backs, 8: tiles
   uint64_t prof_last = __builtin_amdgcn_s_memtime();
 #endif
   int sub = (int)(blockIdx.x % kSub);  // thread 0's dequeue cursor
@@ -844,6 +853,10 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
       const int li = wbase + i * 64;
       e[i] = li < nvalid ? load_elem_nt(in + tb + li) : Elem{0ull, 0ull};
     }
+#ifdef LSB_OS_PROFILE
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    OS_MARK(6);  // tile loads in flight
+#endif
     // Status rows of this sub-array through one buffer descriptor (byte
     // offsets < 2^31); the even lane of a pair publishes and polls buckets
     // t, t + 1 as one 8-byte sc1 access: two self-tagged 4-byte halves,
@@ -857,7 +870,15 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
     constexpr uint32_t kRowBytes = kBuckets * 4;
     const uint32_t my_off = (uint32_t)(tile - first) * kRowBytes + (uint32_t)t * 4u;
     uint32_t prow = (uint32_t)(tile - first) - 1u;  // newest predecessor row not yet summed
-    v2u g = {0u, 0u};
+    // Look-back window: rows prow, prow - 1, ... in flight together.  Rows
+    // before the sub-array's first read as 0 (buffer range check) and are
+    // never consumed: the first row always carries its prefix.
+    v2u g[kLookW];
+    auto load_window = [&]() {
+#pragma unroll
+      for (int r = 0; r < kLookW; ++r)
+        g[r] = __builtin_amdgcn_raw_buffer_load_b64(rs, (prow - (uint32_t)r) * kRowBytes + (uint32_t)t * 4u, 0, 16);
+    };
     uint32_t cnt = 0, lstart;
     // Stable rank of every element among the wave's elements of its digit
     // (per-wave counters), then the tile's counts: publish the aggregate,
@@ -902,8 +923,8 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
     const uint32_t cnt_b = pair_swap(cnt);  // even lanes: lane t + 1's count
     if (even) {
       const uint32_t tg = head ? tag_pre : tag_agg;
-      __builtin_amdgcn_raw_buffer_store_b64(v2u{cnt | tg, cnt_b | tg}, rs, my_off, 0, 16);
-      if (!head) g = __builtin_amdgcn_raw_buffer_load_b64(rs, prow * kRowBytes + (uint32_t)t * 4u, 0, 16);
+      __builtin_amdgcn_raw_buffer_store_b64(v2u{cnt | tg, cnt_b | tg}, rs, my_off, 0, kStPol);
+      if (!head) load_window();
     }
     {
       uint32_t tile_total;
@@ -921,17 +942,30 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
       }
     }
 
+    OS_MARK(3);  // stage
     uint32_t ea = 0, eb = 0;
     if (even && !head) {
       uint32_t spins = 0;
       for (;;) {
-        // Both halves of this launch (parity) and of one kind (prefix bit).
-        if (((g.x ^ g.y) >> 30) == 0 && (g.x & ~kValMask & ~kPreBit) == tag_agg) {
-          ea += g.x & kValMask;
-          eb += g.y & kValMask;
-          if (g.x & kPreBit) break;
-          --prow;
-        } else {
+        // Rows in order, while they are ready: both halves of this launch
+        // (parity) and of one kind (prefix bit); stop at a prefix.
+        uint32_t used = 0;
+        bool done = false;
+#pragma unroll
+        for (int r = 0; r < kLookW; ++r) {
+          if (done || used != (uint32_t)r) continue;
+          if (((g[r].x ^ g[r].y) >> 30) == 0 && (g[r].x & ~kValMask & ~kPreBit) == tag_agg) {
+            ea += g[r].x & kValMask;
+            eb += g[r].y & kValMask;
+            ++used;
+            done = (g[r].x & kPreBit) != 0;
+          }
+        }
+#ifdef LSB_OS_PROFILE
+        if (t == 0) prof[7] += used;
+#endif
+        if (done) break;
+        if (used == 0) {
           __builtin_amdgcn_s_sleep(kPollSleep);
           if ((++spins & 1023u) == 0 &&
               (spins > kSpinLimit ||
@@ -940,10 +974,11 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
             break;
           }
         }
-        g = __builtin_amdgcn_raw_buffer_load_b64(rs, prow * kRowBytes + (uint32_t)t * 4u, 0, 16);
+        prow -= used;
+        load_window();
       }
       __builtin_amdgcn_raw_buffer_store_b64(v2u{(ea + cnt) | tag_pre, (eb + cnt_b) | tag_pre}, rs,
-                                            my_off, 0, 16);
+                                            my_off, 0, kStPol);
     }
     const uint32_t eb_left = pair_swap(eb);  // odd lanes: lane t - 1's sum
     const uint64_t excl = even ? ea : eb_left;
@@ -967,7 +1002,10 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
       cut[t] = c;
     }
     __syncthreads();
-    OS_MARK(3);  // stage + look-back
+    OS_MARK(5);  // look-back (+ run cuts, barrier)
+#ifdef LSB_OS_PROFILE
+    if (t == 0) ++prof[8];
+#endif
     if (t == 0) grab(nxt_tile, nxt_sub);  // in flight during the writes
 
     // The loop is instantiated twice (the launch-uniform `skewed` picks one
@@ -1033,7 +1071,7 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
   if (C16) c16_flush();
 #ifdef LSB_OS_PROFILE
   if (t == 0)
-    for (int k = 0; k < 6; ++k) atomicAdd(&g_os_prof[k], (unsigned long long)prof[k]);
+    for (int k = 0; k < 10; ++k) atomicAdd(&g_os_prof[k], (unsigned long long)prof[k]);
 #endif
   if (NEXT) {
     for (int i = t; i < kSub * kBuckets; i += BLOCK)
@@ -1524,14 +1562,14 @@ hipError_t launch_scatter(const Elem* in, Elem* out, int64_t m, int shift, Chunk
   return hipGetLastError();
 }
 
-hipError_t onesweep_profile(unsigned long long* out6, bool reset) {
+hipError_t onesweep_profile(unsigned long long* out10, bool reset) {
 #ifdef LSB_OS_PROFILE
-  hipError_t e = hipMemcpyFromSymbol(out6, HIP_SYMBOL(g_os_prof), 6 * sizeof(unsigned long long));
+  hipError_t e = hipMemcpyFromSymbol(out10, HIP_SYMBOL(g_os_prof), 10 * sizeof(unsigned long long));
   if (e != hipSuccess || !reset) return e;
-  const unsigned long long z[8] = {};
+  const unsigned long long z[10] = {};
   return hipMemcpyToSymbol(HIP_SYMBOL(g_os_prof), z, sizeof z);
 #else
-  for (int k = 0; k < 6; ++k) out6[k] = 0;
+  for (int k = 0; k < 10; ++k) out10[k] = 0;
   (void)reset;
   return hipErrorNotSupported;
 #endif

@@ -1467,12 +1467,14 @@ int merge_sort(lsb_ctx* c) {
 // tile's predecessors belong to running workgroups.)
 #ifdef LSB_OS_PROFILE
 void os_profile_report() {
-  unsigned long long p[6];
+  unsigned long long p[10];
   if (lsb::onesweep_profile(p, true) != hipSuccess) return;
-  const double tot = (double)(p[0] + p[1] + p[2] + p[3] + p[4]) + 1e-9;
+  const double tot = (double)(p[0] + p[1] + p[2] + p[3] + p[4] + p[5] + p[6]) + 1e-9;
   fprintf(stderr,
-          "os_profile: dequeue %.4f rank %.4f scan %.4f stage+lookback %.4f write %.4f (ticks %.0f)\n",
-          p[0] / tot, p[1] / tot, p[2] / tot, p[3] / tot, p[4] / tot, tot);
+          "os_profile: dequeue %.4f load %.4f rank %.4f scan %.4f stage %.4f lookback %.4f write %.4f "
+          "(ticks %.0f; rows summed per tile %.2f over %llu tiles)\n",
+          p[0] / tot, p[6] / tot, p[1] / tot, p[2] / tot, p[3] / tot, p[5] / tot, p[4] / tot, tot,
+          p[8] ? (double)p[7] / (double)p[8] : 0.0, p[8]);
 }
 #endif
 
