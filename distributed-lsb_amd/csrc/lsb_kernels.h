@@ -110,7 +110,12 @@ hipError_t onesweep_profile(unsigned long long* out10, bool reset);
 struct OnesweepExtra {
   uint64_t* totals = nullptr;
   uint64_t* count16 = nullptr;
+  int halves = 1;  // 2: split stage, 3 workgroups per CU (skewed keys; not with count16)
 };
+// The runtime's choice of OnesweepExtra::halves for a rank, from a digit's
+// sub-array histogram (kOnesweepSubs x 256 counts of m records): 2 when one
+// bucket holds more than 1/32 of the records.
+int onesweep_halves_for(const uint32_t* sub_hist_host, int64_t m);
 hipError_t launch_onesweep(const Elem* in, Elem* out, int64_t m, int shift, int next_shift,
                            const uint32_t* sub_hist, uint32_t* next_hist, uint32_t* status,
                            uint32_t* tile_ctr, uint32_t epoch, uint32_t* err, int grid,

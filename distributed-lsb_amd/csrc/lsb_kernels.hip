@@ -735,8 +735,16 @@ __device__ unsigned long long g_os_prof[10];
 // its tile's low byte changes (a workgroup's tiles are taken in order, so
 // that is a few times per launch).  A tile across a low-byte boundary walks
 // its staged runs.
-template <int BLOCK, int IPT, bool NEXT, bool C16>
-__global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
+//
+// HALVES = 2 (skewed keys, chosen per sort by the runtime): the ranked tile
+// is staged and written in two halves of the tile's output order, so the
+// stage is 32 KiB and 3 workgroups fit a CU instead of 2.  The records stay
+// in registers until their half is staged.  Zipf keys sort 5.7 % faster
+// this way (their serialised next-digit adds hide behind a third
+// workgroup); uniform keys 4.7 % slower (two more barriers per tile, half-
+// length write phases): profiles/ab/r02_ab12_*.
+template <int BLOCK, int IPT, bool NEXT, bool C16, int HALVES>
+__global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_onesweep(
     const Elem* __restrict__ in, Elem* __restrict__ out, int64_t m, int shift, int next_shift,
     const uint32_t* __restrict__ sub_hist, uint32_t* __restrict__ next_hist,
     uint32_t* __restrict__ status, uint32_t* __restrict__ tile_ctr, uint32_t epoch,
@@ -746,7 +754,8 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
   constexpr int T = BLOCK * IPT;
   static_assert(BLOCK == kBuckets, "one thread per bucket in the look-back");
 
-  __shared__ Elem stage[T];                     // the ranked tile (64 KiB)
+  constexpr int HT = T / HALVES;                // staged records per half
+  __shared__ Elem stage[HT];                    // the ranked tile (64 KiB, or one half)
   __shared__ uint32_t wcnt[W][kBuckets];        // per-wave digit counters -> positions
   __shared__ int64_t delta[kBuckets];           // global dest = delta[digit] + tile position
   __shared__ uint32_t cut[NEXT ? kBuckets : 1];  // next-pass sub-array of a run: see below
@@ -773,12 +782,15 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
 
   // Bucket starts (exclusive scan of the digit totals) and this thread's
   // bucket column of the sub-array histogram.
-  uint32_t col[kSub];
+  // (The split-stage form re-reads the column when it changes sub-array,
+  // a few times per launch: its records need the registers.)
+  uint32_t col[HALVES == 1 ? kSub : 1];
   uint64_t tot = 0;
 #pragma unroll
   for (int x = 0; x < kSub; ++x) {
-    col[x] = sub_hist[x * kBuckets + t];
-    tot += col[x];
+    const uint32_t v = sub_hist[x * kBuckets + t];
+    if (HALVES == 1) col[x] = v;
+    tot += v;
   }
   uint64_t all;
   const uint64_t bstart = block_exclusive_scan<BLOCK>(tot, scan64, &all);
@@ -840,7 +852,8 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
       cur_sub = x;
       uint64_t pre = 0;
 #pragma unroll
-      for (int xx = 0; xx < kSub; ++xx) pre += xx < x ? col[xx] : 0u;
+      for (int xx = 0; xx < kSub; ++xx)
+        pre += xx < x ? (HALVES == 1 ? col[xx] : sub_hist[xx * kBuckets + t]) : 0u;
       base = bstart + pre;
     }
     const int64_t tb = (int64_t)tile * T;
@@ -934,13 +947,23 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
     }
     __syncthreads();
     OS_MARK(2);  // publish + scan
+    // Split stage: half 0 turns rk[i] into the record's tile position and
+    // the later half reuses it.
+    auto stage_half = [&](int h) {
 #pragma unroll
-    for (int i = 0; i < IPT; ++i) {
-      if (wbase + i * 64 < nvalid) {
-        const uint32_t d = (uint32_t)(e[i].key >> shift) & (kBuckets - 1);
-        stage[wcnt[w][d] + rk[i]] = e[i];
+      for (int i = 0; i < IPT; ++i) {
+        if (wbase + i * 64 < nvalid) {
+          const uint32_t d = (uint32_t)(e[i].key >> shift) & (kBuckets - 1);
+          if (HALVES == 1) {
+            stage[wcnt[w][d] + rk[i]] = e[i];
+          } else {
+            if (h == 0) rk[i] += wcnt[w][d];
+            if ((int)(rk[i] / HT) == h) stage[rk[i] - h * HT] = e[i];
+          }
+        }
       }
-    }
+    };
+    stage_half(0);
 
     OS_MARK(3);  // stage
     uint32_t ea = 0, eb = 0;
@@ -1010,10 +1033,11 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
 
     // The loop is instantiated twice (the launch-uniform `skewed` picks one
     // outside it): a per-record branch on it cost uniform keys 2.4 %.
-    auto write_out = [&](auto skew_tag) {
+    auto write_out = [&](auto skew_tag, int h) {
       constexpr bool kSkew = decltype(skew_tag)::value;
-      for (int j = t; j < nvalid; j += BLOCK) {
-        const Elem v = stage[j];
+      const int jend = HALVES == 1 || (h + 1) * HT >= nvalid ? nvalid : (h + 1) * HT;
+      for (int j = h * HT + t; j < jend; j += BLOCK) {
+        const Elem v = stage[j - h * HT];
         const uint32_t d = (uint32_t)(v.key >> shift) & (kBuckets - 1);
         const int64_t g = delta[d] + j;
         LSB_DASSERT(g >= 0 && g < m);
@@ -1053,19 +1077,27 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_onesweep(
         }
       }
     };
-    if (skewed) write_out(std::true_type{});
-    else write_out(std::false_type{});
-    if (C16 && mixed16) {  // the tile crosses a low-byte boundary: walk run t
-      for (uint32_t k = 0; k < cnt; ++k) {
-        const uint32_t l = (uint32_t)(stage[lstart + k].key >> shift16) & 0xFFu;
-        if (l != acc_lo) {
-          c16_flush();
-          acc_lo = l;
-        }
-        ++acc;
+    for (int h = 0; h < HALVES; ++h) {
+      if (h > 0) {
+        stage_half(h);
+        __syncthreads();
       }
+      if (skewed) write_out(std::true_type{}, h);
+      else write_out(std::false_type{}, h);
+      if (C16 && mixed16) {  // the tile crosses a low-byte boundary: walk run t
+        const uint32_t k0 = lstart > (uint32_t)(h * HT) ? lstart : (uint32_t)(h * HT);
+        const uint32_t k1 = lstart + cnt < (uint32_t)((h + 1) * HT) ? lstart + cnt : (uint32_t)((h + 1) * HT);
+        for (uint32_t k = k0; k < k1; ++k) {
+          const uint32_t l = (uint32_t)(stage[k - h * HT].key >> shift16) & 0xFFu;
+          if (l != acc_lo) {
+            c16_flush();
+            acc_lo = l;
+          }
+          ++acc;
+        }
+      }
+      __syncthreads();
     }
-    __syncthreads();
     OS_MARK(4);  // write
   }
   if (C16) c16_flush();
@@ -1592,41 +1624,61 @@ hipError_t launch_subhist(const Elem* A, int64_t m, int shift, int grid, uint32_
   return hipGetLastError();
 }
 
+int onesweep_halves_for(const uint32_t* h, int64_t m) {
+  for (int b = 0; b < kBuckets; ++b) {
+    uint64_t tot = 0;
+    for (int x = 0; x < kSub; ++x) tot += h[x * kBuckets + b];
+    if (tot > (uint64_t)(m >> 5)) return 2;  // the kernel's own `skewed` test
+  }
+  return 1;
+}
+
 hipError_t launch_onesweep(const Elem* in, Elem* out, int64_t m, int shift, int next_shift,
                            const uint32_t* sub_hist, uint32_t* next_hist, uint32_t* status,
                            uint32_t* tile_ctr, uint32_t epoch, uint32_t* err, int grid,
                            hipStream_t s, OnesweepExtra extra) {
   if (m <= 0) return hipSuccess;
   if (m > kOnesweepMaxElems || epoch == 0 || epoch >= (1u << 31) || shift < 0 || shift > 56 ||
-      next_shift > 56)
+      next_shift > 56 || (extra.halves != 1 && extra.halves != 2))
     return hipErrorInvalidValue;
   hipError_t e = hipMemsetAsync(tile_ctr, 0, sizeof(uint32_t) * kSub, s);
   if (e != hipSuccess) return e;
   const int64_t TT = (m + kTile - 1) / kTile;
-  // Persistent grid, a multiple of the XCD count; no more than the tiles.
-  int64_t g = grid < kSub ? kSub : grid;
-  if (g > (TT + kSub - 1) / kSub * kSub) g = (TT + kSub - 1) / kSub * kSub;
-  uint32_t* st = status;
   auto* c16 = reinterpret_cast<unsigned long long*>(extra.count16);
+  // The split stage only for the plain and next-digit forms.
+  const bool split = extra.halves == 2 && c16 == nullptr;
+  // Persistent grid (`grid` = 2 workgroups per CU; 3 with the split stage),
+  // a multiple of the XCD count; no more than the tiles.
+  int64_t g = split ? (int64_t)grid * 3 / 2 : grid;
+  if (g < kSub) g = kSub;
+  if (g > (TT + kSub - 1) / kSub * kSub) g = (TT + kSub - 1) / kSub * kSub;
+  const dim3 gd((unsigned)g), bd(kScatterBlock);
+  uint32_t* st = status;
   if (c16) {
     // The 16-bit counts need the low byte below this digit, and no next
     // digit: the exchange follows this pass.
     if (shift < 8 || next_shift >= 0) return hipErrorInvalidValue;
     e = hipMemsetAsync(c16, 0, sizeof(uint64_t) * 65536, s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_onesweep<kScatterBlock, kScatterIpt, false, true>), dim3((unsigned)g),
-                       dim3(kScatterBlock), 0, s, in, out, m, shift, 0, sub_hist, nullptr, st,
-                       tile_ctr, epoch, err, extra.totals, c16);
+    hipLaunchKernelGGL((k_onesweep<kScatterBlock, kScatterIpt, false, true, 1>), gd, bd, 0, s, in, out,
+                       m, shift, 0, sub_hist, nullptr, st, tile_ctr, epoch, err, extra.totals, c16);
   } else if (next_shift >= 0) {
     e = hipMemsetAsync(next_hist, 0, sizeof(uint32_t) * kSub * kBuckets, s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_onesweep<kScatterBlock, kScatterIpt, true, false>), dim3((unsigned)g),
-                       dim3(kScatterBlock), 0, s, in, out, m, shift, next_shift, sub_hist,
-                       next_hist, st, tile_ctr, epoch, err, extra.totals, nullptr);
+    if (split)
+      hipLaunchKernelGGL((k_onesweep<kScatterBlock, kScatterIpt, true, false, 2>), gd, bd, 0, s, in, out,
+                         m, shift, next_shift, sub_hist, next_hist, st, tile_ctr, epoch, err,
+                         extra.totals, nullptr);
+    else
+      hipLaunchKernelGGL((k_onesweep<kScatterBlock, kScatterIpt, true, false, 1>), gd, bd, 0, s, in, out,
+                         m, shift, next_shift, sub_hist, next_hist, st, tile_ctr, epoch, err,
+                         extra.totals, nullptr);
+  } else if (split) {
+    hipLaunchKernelGGL((k_onesweep<kScatterBlock, kScatterIpt, false, false, 2>), gd, bd, 0, s, in, out,
+                       m, shift, 0, sub_hist, nullptr, st, tile_ctr, epoch, err, extra.totals, nullptr);
   } else {
-    hipLaunchKernelGGL((k_onesweep<kScatterBlock, kScatterIpt, false, false>), dim3((unsigned)g),
-                       dim3(kScatterBlock), 0, s, in, out, m, shift, 0, sub_hist, nullptr, st,
-                       tile_ctr, epoch, err, extra.totals, nullptr);
+    hipLaunchKernelGGL((k_onesweep<kScatterBlock, kScatterIpt, false, false, 1>), gd, bd, 0, s, in, out,
+                       m, shift, 0, sub_hist, nullptr, st, tile_ctr, epoch, err, extra.totals, nullptr);
   }
   return hipGetLastError();
 }

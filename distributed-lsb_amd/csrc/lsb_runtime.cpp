@@ -92,6 +92,8 @@ struct Rank {
   uint32_t* os_hist = nullptr;          // [2][8][256] sub-array histograms (ping-pong)
   uint32_t* os_ctr = nullptr;           // [8] tile counters, [8] look-back error word
   uint32_t* os_err_h = nullptr;         // pinned mirror of the error word
+  uint32_t* os_hist_h = nullptr;        // pinned mirror of a sub-array histogram
+  int os_halves = 1;                    // this sort's k_onesweep stage split (1 or 2)
   uint32_t os_epoch = 0;                // last look-back epoch
   int os_grid = 0;                      // persistent grid (2 workgroups per CU)
   // Per-digit exchange with single-read local passes (sort_exchange_onesweep):
@@ -139,6 +141,7 @@ struct lsb_ctx {
   bool peer_ready = false;    // peer tables set up
   bool onesweep = true;       // P == 1: single-read passes (k_subhist + k_onesweep)
   bool self_coll = false;     // the self segment also goes through the collective
+  int os_split = 0;           // LSB_OPT_ONESWEEP_SPLIT: 0 auto, 1 never, 2 always
   int64_t coll_calls = 0, coll_bytes = 0, coll_max = 0;  // element payload handed to the collective
   // What the last lsb_sort ran (lsb_get_last_sort).
   int last_local_passes = 0;
@@ -331,6 +334,7 @@ void free_rank(Rank& r) {
   (void)hipFree(r.os_hist);
   (void)hipFree(r.os_ctr);
   (void)hipHostFree(r.os_err_h);
+  (void)hipHostFree(r.os_hist_h);
   (void)hipFree(r.A);
   (void)hipFree(r.B);
   (void)hipFree(r.R);
@@ -875,6 +879,7 @@ int onesweep_ensure(Rank& r) {
   LSB_TRY(dev_alloc(&r.os_ctr, 2 * lsb::kOnesweepSubs));
   LSB_TRY(host_alloc(&r.os_err_h, 1));
   *r.os_err_h = 0;
+  LSB_TRY(host_alloc(&r.os_hist_h, (size_t)lsb::kOnesweepSubs * lsb::kBuckets));
   HIP_TRY(hipMemsetAsync(r.os_status, 0, tiles * lsb::kBuckets * sizeof(uint32_t), r.stream));
   HIP_TRY(hipMemsetAsync(r.os_ctr, 0, 2 * lsb::kOnesweepSubs * sizeof(uint32_t), r.stream));
   r.os_epoch = 0;
@@ -887,6 +892,27 @@ int onesweep_ensure(Rank& r) {
 // only the alternation matters (the counter runs on for the record).
 int next_epoch(Rank& r) {
   if (++r.os_epoch >= (1u << 30)) r.os_epoch = 2;  // 2^30 is even: keep the alternation
+  return LSB_OK;
+}
+
+// This sort's k_onesweep stage split for rank r (LSB_OPT_ONESWEEP_SPLIT).
+// Auto decides from the first digit's sub-array histogram (`hist`, on
+// r.stream): queue_halves queues its 8 KiB read-back, to share the span's
+// stream sync; choose_halves decides after that sync.
+int queue_halves(lsb_ctx* c, Rank& r, const uint32_t* hist) {
+  if (c->os_split != 0 || r.here == 0) return LSB_OK;
+  HIP_TRY(hipMemcpyAsync(r.os_hist_h, hist, sizeof(uint32_t) * lsb::kOnesweepSubs * lsb::kBuckets,
+                         hipMemcpyDeviceToHost, r.stream));
+  return LSB_OK;
+}
+
+int choose_halves(lsb_ctx* c, Rank& r, bool synced) {
+  if (c->os_split != 0 || r.here == 0) {
+    r.os_halves = c->os_split == 2 ? 2 : 1;
+    return LSB_OK;
+  }
+  if (!synced) HIP_TRY(hipStreamSynchronize(r.stream));
+  r.os_halves = lsb::onesweep_halves_for(r.os_hist_h, r.here);
   return LSB_OK;
 }
 
@@ -907,6 +933,7 @@ int sort_onesweep_rank(lsb_ctx* c, Rank& r, int* passes, uint64_t* varying) {
     HIP_TRY(lsb::launch_subhist(r.A, m, 0, r.os_grid, hist[0], c->skip_constant ? r.span : nullptr,
                                 r.stream));
   }
+  LSB_TRY(queue_halves(c, r, hist[0]));
   std::vector<int> digits{0};
   *varying = ~0ull;
   *passes = 0;
@@ -915,6 +942,7 @@ int sort_onesweep_rank(lsb_ctx* c, Rank& r, int* passes, uint64_t* varying) {
     HIP_TRY(hipStreamSynchronize(r.stream));
     *varying = r.span_h[0] & r.span_h[1];
   }
+  LSB_TRY(choose_halves(c, r, c->skip_constant));
   for (int d = 1; d < 64 / lsb::kDigitBits; ++d)
     if (((*varying >> (d * lsb::kDigitBits)) & (lsb::kBuckets - 1)) != 0) digits.push_back(d);
   for (size_t i = 0; i < digits.size(); ++i) {
@@ -923,9 +951,11 @@ int sort_onesweep_rank(lsb_ctx* c, Rank& r, int* passes, uint64_t* varying) {
     LSB_TRY(next_epoch(r));
     {
       Timer t(c, &r, LSB_K_SCATTER);
+      lsb::OnesweepExtra x;
+      x.halves = r.os_halves;
       HIP_TRY(lsb::launch_onesweep(r.A, r.B, m, shift, next, hist[i & 1], hist[(i + 1) & 1],
                                    r.os_status, r.os_ctr, r.os_epoch,
-                                   r.os_ctr + lsb::kOnesweepSubs, r.os_grid, r.stream));
+                                   r.os_ctr + lsb::kOnesweepSubs, r.os_grid, r.stream, x));
       if (c->timing) c->scatter_elems += m;
     }
     std::swap(r.A, r.B);
@@ -962,6 +992,7 @@ bool exchange_onesweep_applies(const lsb_ctx* c) {
 // byte at `next` over the output (the next local pass follows directly).
 int local_pass_os(lsb_ctx* c, Rank& r, int shift, int next, lsb::OnesweepExtra extra) {
   HIP_TRY(hipSetDevice(r.dev));
+  extra.halves = r.os_halves;
   r.starts_fused = false;
   const int64_t m = r.here;
   if (m == 0) {
@@ -1009,12 +1040,18 @@ int sort_exchange_onesweep(lsb_ctx* c) {
                                   c->skip_constant ? r.span : nullptr, r.stream));
       r.os_valid = 0;
     }
+    LSB_TRY(queue_halves(c, r, r.os_hist));
   }
   uint64_t varying = ~0ull;
   if (c->skip_constant) {
     uint64_t kor = 0, knor = 0;
     LSB_TRY(gather_span(c, &kor, &knor));
     varying = kor & knor;
+  }
+  // gather_span syncs only the streams it reads from: each rank syncs here.
+  for (Rank& r : c->ranks) {
+    HIP_TRY(hipSetDevice(r.dev));
+    LSB_TRY(choose_halves(c, r, false));
   }
   c->last_varying = varying;
   // Local passes in order; an exchange follows the last one of each digit.
@@ -1735,6 +1772,10 @@ int lsb_set_option(lsb_ctx_t* c, int option, int64_t value) {
       return LSB_OK;
     case LSB_OPT_EXCHANGE_SELF:
       c->self_coll = value != 0;
+      return LSB_OK;
+    case LSB_OPT_ONESWEEP_SPLIT:
+      if (value < 0 || value > 2) return fail(LSB_ERR_INVALID, "lsb_set_option", "split must be 0..2");
+      c->os_split = (int)value;
       return LSB_OK;
     case LSB_OPT_EXCHANGE_SLICES:
       if (value < 1 || value > 64)

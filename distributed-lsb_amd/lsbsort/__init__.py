@@ -49,6 +49,7 @@ OPT_TIMING, OPT_FORCE_EXCHANGE, OPT_SKIP_CONSTANT_DIGITS, OPT_EXCHANGE_SLICES, O
 OPT_EXCHANGE_PEER = 5
 OPT_ONESWEEP = 6
 OPT_EXCHANGE_SELF = 7
+OPT_ONESWEEP_SPLIT = 8
 
 
 class LsbError(RuntimeError):

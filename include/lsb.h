@@ -94,6 +94,11 @@ typedef struct lsb_ctx lsb_ctx_t;
                                       buffer like every other source; 0 (default) places it
                                       straight out of A.  Same output; lets a world of one
                                       carry the whole payload through RCCL (tests). */
+#define LSB_OPT_ONESWEEP_SPLIT  8  /* single-read passes' LDS stage: 0 (default) chosen per
+                                      sort from the first digit's histogram (one bucket over
+                                      1/32 of a rank's records: the tile is staged in two
+                                      halves, 3 workgroups per CU); 1 never split; 2 always
+                                      split.  Same output. */
 
 /* ---- geometry: DistributedArray::create (mpi/mpi_lsbsort.cpp:144-149) ---- */
 int64_t lsb_per_rank(int64_t n_total, int num_ranks);            /* ceil(n/P) */

@@ -23,9 +23,10 @@ pytestmark = pytest.mark.gpu
 T = 4096
 
 
-def _sort(lsbsort, a, P, bits, onesweep, slices=0, peer=0, skip=1, stats=False):
+def _sort(lsbsort, a, P, bits, onesweep, slices=0, peer=0, skip=1, stats=False, split=0):
     with lsbsort.World(a.size, ranks=P, radix_bits=bits) as w:
         w.set_option(lsbsort.OPT_ONESWEEP, onesweep)
+        w.set_option(lsbsort.OPT_ONESWEEP_SPLIT, split)
         w.set_option(lsbsort.OPT_SKIP_CONSTANT_DIGITS, skip)
         if slices:
             w.set_option(lsbsort.OPT_EXCHANGE_SLICES, slices)
@@ -72,6 +73,22 @@ def test_distributions_bit_exact(lsb_built, oracle_mod, name, P, bits):
     for skip in (1, 0):
         out, _, _ = _sort(lsb_built, a, P, bits, 1, skip=skip)
         assert np.array_equal(out, oracle_mod.stable_sort(a)), skip
+
+
+@pytest.mark.parametrize("split", [1, 2])
+@pytest.mark.parametrize("name", ["uniform", "zipf", "hot_bucket"])
+@pytest.mark.parametrize("P,bits", [(2, 16), (3, 8)])
+def test_split_stage(lsb_built, oracle_mod, name, P, bits, split):
+    """Both k_onesweep stage forms in every rank's local passes (the 16-bit
+    digit's high-byte pass, which counts the 65536 digits, keeps the whole
+    stage)."""
+    n = 200_003
+    if name == "uniform":
+        a = _uniform(n, 99 + split)
+    else:
+        a = _dist(name, n, np.random.default_rng(hash((name, P, split)) & 0xFFFF))
+    out, _, _ = _sort(lsb_built, a, P, bits, 1, split=split)
+    assert np.array_equal(out, oracle_mod.stable_sort(a))
 
 
 @pytest.mark.parametrize("slices", [1, 3, 8])

@@ -17,10 +17,11 @@ pytestmark = pytest.mark.gpu
 T = 4096
 
 
-def _sort(lsbsort, a, onesweep, skip=1):
+def _sort(lsbsort, a, onesweep, skip=1, split=0):
     with lsbsort.World(a.size, ranks=1) as w:
         w.set_option(lsbsort.OPT_ONESWEEP, onesweep)
         w.set_option(lsbsort.OPT_SKIP_CONSTANT_DIGITS, skip)
+        w.set_option(lsbsort.OPT_ONESWEEP_SPLIT, split)
         w.copy_in(0, a)
         w.my_sort()
         w.sync()
@@ -57,6 +58,37 @@ def test_distributions_bit_exact(lsb_built, oracle_mod, name, n):
     for skip in (1, 0):
         out, _ = _sort(lsb_built, a, 1, skip)
         assert np.array_equal(out, oracle_mod.stable_sort(a)), skip
+
+
+@pytest.mark.parametrize("split", [1, 2])
+@pytest.mark.parametrize("n", [1, T // 2 - 1, T // 2, T // 2 + 1, T + T // 2, 8 * T + 1,
+                               17 * T + 2049, 100_003])
+def test_split_stage_sizes(lsb_built, oracle_mod, n, split):
+    """LSB_OPT_ONESWEEP_SPLIT forced: the tile staged whole (1) or in two
+    halves of its output order (2, 3 workgroups per CU), around half-tile
+    boundaries and partial tiles."""
+    a = _uniform(n, 7 * n + split)
+    out, _ = _sort(lsb_built, a, 1, split=split)
+    assert np.array_equal(out, oracle_mod.stable_sort(a))
+
+
+@pytest.mark.parametrize("split", [1, 2])
+@pytest.mark.parametrize("name", ["all_equal", "two_keys", "hot_bucket", "zipf", "sorted",
+                                  "reverse"])
+def test_split_stage_distributions(lsb_built, oracle_mod, name, split):
+    """Skewed keys through both stage forms (auto picks the split one for
+    them); runs of one bucket cross the half-stage boundary."""
+    n = 300_001
+    rng = np.random.default_rng(hash((name, split)) & 0xFFFF)
+    a = _dist(name, n, rng)
+    out, _ = _sort(lsb_built, a, 1, split=split)
+    assert np.array_equal(out, oracle_mod.stable_sort(a))
+
+
+def test_split_option_rejected(lsb_built):
+    with lsb_built.World(1000, ranks=1) as w:
+        with pytest.raises(lsb_built.LsbError):
+            w.set_option(lsb_built.OPT_ONESWEEP_SPLIT, 3)
 
 
 def test_one_bucket_per_subarray(lsb_built, oracle_mod):

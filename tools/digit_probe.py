@@ -16,6 +16,8 @@ n = 1 << lg
 # LSB_RADIX_BITS=16 and LSB_FORCE_EXCHANGE=1: the per-digit exchange path at
 # P = 1 (counts, plan, k_place), as tools/exchange_profile.py, with LSB_DIST keys.
 w = lsbsort.World(n, 1, radix_bits=int(os.environ.get("LSB_RADIX_BITS", "8")))
+if os.environ.get("LSB_SPLIT"):  # LSB_OPT_ONESWEEP_SPLIT: 0 auto, 1 never, 2 always
+    w.set_option(lsbsort.OPT_ONESWEEP_SPLIT, int(os.environ["LSB_SPLIT"]))
 if os.environ.get("LSB_FORCE_EXCHANGE") == "1":
     w.set_option(lsbsort.OPT_FORCE_EXCHANGE, 1)
 # LSB_PASSES=reduce-scan: count + scan + scatter per pass instead of single-read passes

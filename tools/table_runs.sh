@@ -7,7 +7,7 @@ cd $R
 : > gpurun_out/table.log
 for args in "" "--passes reduce-scan" "--dist zipf" "--radix-bits 16" "--n-per-gpu 4294967296 --steps 3 --warmup 1"; do
   echo "args: $args" >> gpurun_out/table.log
-  timeout -k 10 300 python -u bench.py --no-cpu-baseline $args >> gpurun_out/table.log 2>&1 || exit 1
+  timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-traffic $args >> gpurun_out/table.log 2>&1 || exit 1
 done
 python3 - <<'PY'
 import json
