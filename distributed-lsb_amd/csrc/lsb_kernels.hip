@@ -597,8 +597,11 @@ constexpr int kPollSleep = 1;              // s_sleep between look-back polls (4
 // slow every poll).
 constexpr int kLookW = 1;
 // Status stores write through (sc1): plain stores stay dirty in the
-// writer's L2 and a poller never saw them (look-back timed out,
-// gpurun_out/ab10).
+// writer's L2 and a poller on another XCD never sees them (look-back timed
+// out).  Keeping every chain on its own XCD (tiles by XCC_ID, no helping)
+// made plain stores work but not faster: a poll's round trip is queueing in
+// the polling CU's memory pipeline, not the L2 miss
+// (profiles/ab/r02_ab15_uniform.log).
 constexpr int kStPol = 16;
 
 typedef __attribute__((address_space(1))) uint32_t gu32;
