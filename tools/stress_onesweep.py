@@ -19,11 +19,12 @@ def main():
     ap.add_argument("--n", type=int, default=1 << 26)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--tag", default="")
+    ap.add_argument("--dist", choices=("uniform", "zipf"), default="uniform")  # zipf: split stage
     a = ap.parse_args()
     bad = 0
     with lsbsort.World(a.n, ranks=1) as w:
         for i in range(a.iters):
-            w.generate()
+            w.generate(a.dist)
             try:
                 w.my_sort()
                 w.sync()
