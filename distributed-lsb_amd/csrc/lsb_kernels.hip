@@ -1,11 +1,19 @@
 // HIP kernels of the MI355X-native LSD radix sort (gfx950 / CDNA4).
 //
-// One local pass on one 8-bit digit, per rank, is reduce-then-scan:
-//   k_upsweep  per-chunk digit histogram         (count loop, mpi/mpi_lsbsort.cpp:226-229)
+// A sort's local passes (localShuffle, mpi/mpi_lsbsort.cpp:213-247) read
+// each record once per pass:
+//   k_subhist  the first digit's histogram per sub-array, once per sort
+//              (count loop :226-229), plus the key span
+//   k_onesweep count + scan + stable scatter of one 8-bit digit in one read
+//              (:226-246): offsets by decoupled look-back, and the next
+//              digit's histogram counted as the records are written
+// The reduce-then-scan form of the same pass (lsb_pass, LSB_OPT_ONESWEEP = 0):
+//   k_upsweep  per-chunk digit histogram         (count loop, :226-229)
 //   k_scan     chunk x bucket exclusive scan      (starts, :232-238 / exclusiveScan :385-414)
 //   k_scatter  stable scatter through LDS         (shuffle loop, :241-246)
 // and, when P > 1, after the RCCL exchange,
-//   k_place    received runs -> final local slots (placement loop, :568-575)
+//   k_place    received runs -> final local slots (placement loop, :568-575),
+//              counting the next local digit's histogram as it writes
 //
 // Everything is integer indexing, so the bound is HBM, not MFMA.  Design
 // points for CDNA4:
