@@ -436,6 +436,19 @@ def test_large_verify_on_device(lsb_built, n, P):
         assert w.check_sorted()
 
 
+@pytest.mark.parametrize("split", [0, 1, 2])
+@pytest.mark.parametrize("n,P,bits", [((1 << 27) + 333, 1, 8), ((1 << 26) + 12345, 2, 16)])
+def test_large_zipf_verify_on_device(lsb_built, n, P, bits, split):
+    """Zipf keys at scale through every stage form (auto picks the split
+    stage for them), at P = 1 and through the per-digit exchange."""
+    with lsb_built.World(n, ranks=P, radix_bits=bits) as w:
+        w.set_option(lsb_built.OPT_ONESWEEP_SPLIT, split)
+        w.generate("zipf", 1.1)
+        w.my_sort()
+        assert w.verify() == (True, -1)
+        assert w.check_sorted()
+
+
 def test_beyond_32bit_indices(lsb_built):
     """2^32 + 12345 records on one rank (137 GB of A + B): every index,
     chunk offset and bucket start must be 64-bit (the reference's int MPI
