@@ -3,7 +3,7 @@
 # (live PMC traffic + CPU baseline), rocprofv3 kernel stats and FETCH/WRITE.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=$R/gpurun_out/r02final
+O=$R/gpurun_out/${OUT:-r02final}
 mkdir -p $O
 cd $R
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gputests.log 2>&1 \
