@@ -72,9 +72,11 @@ def parse():
                          "whole key: local sort, ONE all-to-all, merge); default 8 on 1 GPU, 16 on "
                          ">1 GPU; local passes are 8-bit either way")
     ap.add_argument("--dist", choices=("uniform", "zipf"), default="uniform")
-    ap.add_argument("--transport", choices=("rccl", "gloo"), default="rccl",
-                    help="N > 1 collectives: RCCL over xGMI (the measurement), or gloo host "
-                         "callbacks (lsb_create_rank_ops) to rehearse the flow on fewer GPUs")
+    ap.add_argument("--transport", choices=("rccl", "rccl-sockets", "gloo"), default="rccl",
+                    help="N > 1 collectives: RCCL over xGMI (the measurement); RCCL between ranks "
+                         "that share GPUs, one NCCL_HOSTID per rank so RCCL links them by its socket "
+                         "transport (a rehearsal of the RCCL path on fewer GPUs); or gloo host "
+                         "callbacks (lsb_create_rank_ops)")
     ap.add_argument("--exchange", choices=("alltoallv", "p2p", "peer"), default="alltoallv",
                     help="N > 1 element exchange: RCCL AllToAllv in slices (default), grouped "
                          "ncclSend/ncclRecv, or direct peer stores into the owners' buffers")
@@ -330,8 +332,11 @@ def cpu_baseline(gpu_n, cpu_n=0, runs=3):
 def parallelism(N, radix, a):
     if N == 1:
         return "1 GPU, no exchange"
-    if a.transport != "rccl":
+    if a.transport == "gloo":
         return f"{N} ranks, gloo host collectives (rehearsal, not a measurement)"
+    if a.transport == "rccl-sockets":
+        return (f"{N} ranks, RCCL between ranks sharing GPUs over its socket transport "
+                f"(rehearsal of the RCCL path, not a measurement)")
     if radix == 64:
         return (f"block partition over {N} GPUs; local sort per GPU, splitter search (8 RCCL AllGathers "
                 f"of candidate counts), one RCCL " + ("AllToAllv" if a.exchange == "alltoallv" else
@@ -352,9 +357,16 @@ def make_world(a, d, N, n_total, radix):
                                    radix_bits=radix)
     elif d.world > 1:
         device = d.local_rank
+        if a.transport == "rccl-sockets":
+            # Ranks may share a GPU: RCCL accepts that only across "hosts",
+            # so each rank is its own host and the wire is a loopback socket.
+            os.environ["NCCL_HOSTID"] = f"lsb-bench-rank-{d.rank}"
+            os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+            os.environ.setdefault("NCCL_IB_DISABLE", "1")
+            device = d.local_rank % max(1, visible_devices())
         uid = lsbsort.get_unique_id() if d.rank == 0 else None
         uid = d.bcast_bytes(uid)
-        w = lsbsort.World.rank(n_total, N, d.rank, d.local_rank, uid, radix_bits=radix)
+        w = lsbsort.World.rank(n_total, N, d.rank, device, uid, radix_bits=radix)
     else:
         if N != 1:
             raise SystemExit("multi-GPU runs are launched one process per GPU (torch.distributed.run)")

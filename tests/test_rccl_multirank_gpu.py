@@ -1,0 +1,51 @@
+"""The multi-GPU data path between REAL RCCL ranks, on the one GPU we have.
+
+RCCL refuses two ranks of one host on one device, but it decides "one host"
+by NCCL_HOSTID when that is set.  tools/rccl_two_ranks.py starts P processes
+on the GPU, each with its own NCCL_HOSTID, so RCCL connects them with its
+socket transport over loopback.  Every collective of the N > 1 path then runs
+between real ranks with non-empty peer segments: the counts ncclAllGather,
+the sliced ncclAllToAllv or grouped ncclSend/ncclRecv of the records
+(mpi/mpi_lsbsort.cpp:316-324, :563), the span all-gather, the whole-key
+form's splitter-search all-gathers, verify's all-reduce.  The output must be
+the reference's golden digest for `mpirun -n P mpi_lsbsort --n n`.
+
+The wire here is a socket, not xGMI, so nothing is timed.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TOOL = os.path.join(ROOT, "tools", "rccl_two_ranks.py")
+
+
+def _run(bits, n, world, exchange="alltoallv", slices=0):
+    p = subprocess.run([sys.executable, "-u", TOOL, str(bits), str(n), str(world), exchange, str(slices)],
+                       capture_output=True, text=True, timeout=240, cwd=ROOT)
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert lines, f"rc={p.returncode}\n{p.stdout[-2000:]}\n{p.stderr[-2000:]}"
+    return p.returncode, json.loads(lines[-1])
+
+
+@pytest.mark.parametrize("bits,n,world,exchange,slices", [
+    (8, 1_000_000, 2, "alltoallv", 0),
+    (16, 1_000_000, 2, "p2p", 1),
+    (16, 1_000_003, 4, "alltoallv", 7),
+    (64, 1_000_003, 4, "p2p", 0),
+    (16, 1_048_576, 8, "alltoallv", 0),
+    (64, 1_048_576, 8, "alltoallv", 0),
+])
+def test_real_rccl_ranks_golden(lsb_built, bits, n, world, exchange, slices):
+    rc, r = _run(bits, n, world, exchange, slices)
+    assert r["status"] == "ok", r
+    assert r["golden_match"] is True, r
+    assert all(r["verify"]) and all(r["check_sorted"]), r
+    # every rank handed records to RCCL (its peers' segments are non-empty)
+    assert all(b > 0 for b in r["rccl_bytes"]), r
+    assert rc == 0
