@@ -25,6 +25,10 @@
 //   --exchange alltoallv|p2p|peer  element exchange (default RCCL AllToAllv in
 //              slices; grouped Send/Recv; direct peer stores, the shmem_putmem form)
 //   --slices S  all-to-all slices whose placement overlaps the next slice
+//   --share-gpus G  with --gpus P: rank r runs on device r % G and is its own
+//              RCCL "host" (NCCL_HOSTID), so RCCL links ranks that share a GPU
+//              by its socket transport -- a rehearsal of the multi-GPU path on
+//              fewer GPUs (RCCL refuses two ranks of one host on one device)
 #include <sys/wait.h>
 #include <unistd.h>
 
@@ -56,6 +60,7 @@ struct Options {
   int exchange_option = -1;  // --exchange: LSB_OPT_EXCHANGE_P2P / _PEER, or -1 (AllToAllv)
   int slices = 0;            // --slices S (0: library default)
   int64_t test_corrupt = -1; // --test-corrupt I: overwrite sorted record I (tests the report)
+  int share_gpus = 0;        // --share-gpus G: rank r on device r % G, one RCCL host per rank
 };
 
 void flush_output() {
@@ -244,6 +249,16 @@ int run(World& w, const Options& o) {
 }
 
 int run_rank_process(const Options& o, int rank, int read_fd, const std::vector<int>& write_fds) {
+  int dev = rank;
+  if (o.share_gpus > 0) {
+    // Before anything touches RCCL: one host per rank, linked over loopback.
+    char host[64];
+    snprintf(host, sizeof host, "hip-lsbsort-rank-%d", rank);
+    setenv("NCCL_HOSTID", host, 1);
+    setenv("NCCL_SOCKET_IFNAME", "lo", 0);
+    setenv("NCCL_IB_DISABLE", "1", 0);
+    dev = rank % o.share_gpus;
+  }
   unsigned char id[LSB_UNIQUE_ID_BYTES];
   if (rank == 0) {
     CHECK(lsb_get_unique_id(id));
@@ -263,8 +278,8 @@ int run_rank_process(const Options& o, int rank, int read_fd, const std::vector<
   w.per = lsb_per_rank(o.n, o.gpus);
   w.first = rank;
   w.nlocal = 1;
-  w.dev = rank;
-  CHECK(lsb_create_rank(&w.ctx, o.n, o.gpus, rank, rank, o.radix_bits, id));
+  w.dev = dev;
+  CHECK(lsb_create_rank(&w.ctx, o.n, o.gpus, rank, dev, o.radix_bits, id));
   const int status = run(w, o);
   lsb_destroy(w.ctx);
   return status;
@@ -295,6 +310,7 @@ int main(int argc, char* argv[]) {
     else if (a == "--zipf-s") o.zipf_s = std::stod(next());
     else if (a == "--slices") o.slices = std::stoi(next());
     else if (a == "--test-corrupt") o.test_corrupt = std::stoll(next());
+    else if (a == "--share-gpus") o.share_gpus = std::stoi(next());
     else if (a == "--exchange") {
       const std::string x = next();
       if (x == "alltoallv") o.exchange_option = -1;
@@ -311,7 +327,7 @@ int main(int argc, char* argv[]) {
   }
   if (!o.verify_set) o.verify = (o.n < 128LL * 1024 * 1024);
   if (o.radix_bits == 0) o.radix_bits = o.gpus > 1 ? 16 : 8;
-  if (o.n < 0 || o.ranks < 1 || o.gpus < 0) {
+  if (o.n < 0 || o.ranks < 1 || o.gpus < 0 || o.share_gpus < 0) {
     fprintf(stderr, "invalid arguments\n");
     return 2;
   }

@@ -591,3 +591,25 @@ def test_harness_reports_every_mismatch(lsb_built, oracle_mod, mode):
     assert lines[i + 2] == f"Got:      (0123456789abcdef,{n + 7})"
     assert sum(l.startswith("Sorted element ") for l in lines) == 1
     assert "Array is NOT sorted" in lines or "Array is sorted" in lines
+
+
+@pytest.mark.parametrize("n,P,extra", [(1000003, 4, []), (1000000, 2, ["--radix-bits", "64"]),
+                                       (17, 8, ["--exchange", "p2p"])])
+def test_harness_rccl_ranks_share_gpu(lsb_built, ref_vectors, n, P, extra):
+    """`hip_lsbsort --gpus P` forks P RCCL ranks itself; --share-gpus 1 puts
+    them all on this GPU, each its own RCCL host (socket transport), so the
+    harness's multi-process RCCL path prints the reference's own lines."""
+    case = next(c for c in ref_vectors["cases"] if c["n"] == n and c["P"] == P)
+    r = subprocess.run([lsb_built.HARNESS_PATH, "--n", str(n), "--gpus", str(P), "--share-gpus", "1",
+                        "--print", "--verify"] + extra, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    # RCCL prints its own init banner (RCCL / HIP / ROCm versions, ...) to
+    # stdout from rank 0 on some setups, before the harness's first line.
+    lines = r.stdout.splitlines()
+    head = f"Total number of HIP ranks: {P}"
+    assert head in lines, r.stdout[:2000]
+    lines = lines[lines.index(head):]
+    assert lines[1] == f"Problem size: {n}"
+    assert "Array is sorted" in lines
+    printed = [l for l in lines if l.startswith("A[")]
+    assert printed == [f"A[{i}] = ({k},{v})" for i, k, v in case["input"] + case["output"]]
