@@ -111,12 +111,16 @@ class Dist:
             self.dist.barrier()
 
     def max(self, x):
+        return self.max_list([x])[0]
+
+    def max_list(self, xs):
+        """Element-wise max over ranks."""
         if not self.dist:
-            return x
+            return list(xs)
         import torch
-        t = torch.tensor([x], dtype=torch.float64)
+        t = torch.tensor(list(xs), dtype=torch.float64)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
-        return float(t.item())
+        return [float(v) for v in t.tolist()]
 
     def all_true(self, ok):
         if not self.dist:
@@ -383,7 +387,8 @@ def make_world(a, d, N, n_total, radix):
 def timed_sorts(w, d, a, steps, warmup):
     """`warmup` untimed sorts, then `steps` timed ones; each step regenerates
     the input (untimed) and times the sort between barrier + synchronize
-    brackets.  Returns (max-over-ranks total seconds, verified or None)."""
+    brackets.  Returns (max-over-ranks total seconds, verified or None,
+    per-step max-over-ranks seconds)."""
     def step():
         w.generate(a.dist, a.zipf_s)
         w.barrier()
@@ -400,15 +405,13 @@ def timed_sorts(w, d, a, steps, warmup):
         step()
     w.reset_kernel_stats()
     w.set_timing(True)
-    total = 0.0
-    for _ in range(steps):
-        total += step()
+    times = [step() for _ in range(steps)]
     w.set_timing(False)
     verified = None
     if not a.no_verify:
         ok, _ = w.verify()
         verified = d.all_true(ok)
-    return d.max(total), verified
+    return d.max(sum(times)), verified, d.max_list(times)
 
 
 def probe(a):
@@ -439,7 +442,7 @@ def main():
     # counts the next pass's histogram) and each rank of the whole-key form.
     kernel = "k_onesweep" if a.passes == "onesweep" else "k_scatter"
 
-    total, verified = timed_sorts(w, d, a, a.steps, a.warmup)
+    total, verified, step_s = timed_sorts(w, d, a, a.steps, a.warmup)
     stats = w.kernel_stats()
     scatter_elems = w.scatter_elems()
     xcalls, xbytes, _ = w.exchange_bytes()
@@ -488,6 +491,12 @@ def main():
     # single-read passes).
     per_elem = (SCATTER_BYTES_PER_ELEM * launches + COUNT_BYTES_PER_ELEM * stats["upsweep"][0]) / a.steps
     sort_gbs = per_elem * (n_total / N) / (ms_per_step / 1e3) / 1e9
+    # SURVEY.md §8(d)'s sort-level figure: 48 B per record per digit pass
+    # (16 B histogram read + 32 B scatter) over D = 64 / radix_bits passes,
+    # a fixed denominator whatever the design moves (measured bytes: roofline).
+    D = 64 // radix if radix != 64 else 8
+    med_s = sorted(step_s)[len(step_s) // 2]
+    survey_frac = 48 * D * (n_total / N) / med_s / (HBM_PEAK_GBS * 1e9)
     out = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -514,6 +523,11 @@ def main():
                    "parallelism": parallelism(N, radix, a)},
         "roofline": roof,
         "sort_hbm_frac": round(sort_gbs / HBM_PEAK_GBS, 4),
+        "step_ms": [round(t * 1e3, 3) for t in step_s],
+        "median_melem_s": round(n_total / med_s / 1e6, 2),
+        "survey_roofline": {"frac": round(survey_frac, 4), "bytes_per_elem": 48 * D, "passes": D,
+                            "basis": "SURVEY.md 8(d): 48*D*n / (t_sort * P * 8e12), fixed denominator, "
+                                     "median step"},
         "kernel_ms_per_step": {k: round(v[1] / a.steps, 3) for k, v in stats.items()},
         "kernel_ms_per_step_legend": {
             "upsweep": "count read (k_subhist once per sort, or k_upsweep per pass)",
@@ -535,7 +549,7 @@ def main():
         try:
             wk, _ = make_world(a, d, N, n_total, 64)
             k = min(a.steps, 3)
-            wt, wv = timed_sorts(wk, d, a, k, 1)
+            wt, wv, _ = timed_sorts(wk, d, a, k, 1)
             wk.close()
             out["whole_key_melem_s"] = round(n_total * k / wt / 1e6, 2)
             out["whole_key_ms_per_step"] = round(wt / k * 1e3, 3)
