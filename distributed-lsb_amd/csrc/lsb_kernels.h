@@ -23,6 +23,16 @@ constexpr int kBuckets = 1 << kDigitBits;     // 256
 constexpr int kScatterBlock = LSB_SCATTER_BLOCK;  // 4 waves
 constexpr int kScatterIpt = LSB_SCATTER_IPT;      // items per thread
 constexpr int kTile = kScatterBlock * kScatterIpt;  // 4096 elements = 64 KiB in LDS
+#ifndef LSB_OS_BLOCK
+#define LSB_OS_BLOCK 512
+#endif
+// k_onesweep workgroups: 8 waves x 8 records for the whole stage (2 per CU),
+// 4 waves x 16 for the split stage (3 per CU; at 8 waves its registers spill).
+constexpr int kOsBlock = LSB_OS_BLOCK;
+constexpr int kOsIpt = kTile / kOsBlock;
+constexpr int kOsSplitBlock = 256;
+constexpr int kOsSplitIpt = kTile / kOsSplitBlock;
+static_assert(kOsBlock % kBuckets == 0 && kOsBlock * kOsIpt == kTile, "onesweep tile shape");
 constexpr int kMaxChunks = 65536;             // upper bound on the chunk grid
 
 // A rank's `m` elements are cut into `num_chunks` contiguous chunks of

@@ -594,6 +594,12 @@ __global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_scatter(const Elem* __re
 //   * NEXT: the pass also accumulates the sub-array histogram of the next
 //     digit over its OUTPUT positions (the next pass's sub-arrays), in LDS,
 //     one add per record, flushed with global atomics at the end.
+//   * Workgroup shape: the 64 KiB stage holds a CU to 2 workgroups, so the
+//     whole-stage form runs 8 waves x 8 records (kOsBlock = 512; threads
+//     t < 256 own bucket t, the rest only load, rank, stage and write): the
+//     rank chains are half as long and twice the waves hide them, -2.8 % per
+//     sort against 4 waves x 16 (profiles/ab/r02_ab27_*).  The split stage
+//     keeps 4 waves x 16: at 3 workgroups per CU, 8 waves spill.
 // The first pass of a sort takes its sub-array histogram (and the key span)
 // from k_subhist: one read per sort instead of one per pass.
 constexpr int kSub = kOnesweepSubs;
@@ -763,11 +769,16 @@ __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_
     unsigned long long* __restrict__ count16) {
   constexpr int W = BLOCK / 64;
   constexpr int T = BLOCK * IPT;
-  static_assert(BLOCK == kBuckets, "one thread per bucket in the look-back");
+  // Thread t < 256 owns bucket t (counts, scan, look-back, offsets); with
+  // BLOCK = 512 the other threads only load, rank, stage and write.
+  static_assert(BLOCK % kBuckets == 0, "bucket threads");
+  // Per-wave digit counters -> tile positions (< 4096): 16-bit at 8 waves,
+  // so the counters of two workgroups still fit a CU beside their stages.
+  using WC = typename std::conditional<(W > 4), uint16_t, uint32_t>::type;
 
   constexpr int HT = T / HALVES;                // staged records per half
   __shared__ Elem stage[HT];                    // the ranked tile (64 KiB, or one half)
-  __shared__ uint32_t wcnt[W][kBuckets];        // per-wave digit counters -> positions
+  __shared__ WC wcnt[W][kBuckets];              // per-wave digit counters -> positions
   __shared__ int64_t delta[kBuckets];           // global dest = delta[digit] + tile position
   __shared__ uint32_t cut[NEXT ? kBuckets : 1];  // next-pass sub-array of a run: see below
   __shared__ uint32_t nh[NEXT ? kSub * kBuckets : 1];  // next digit's sub-array histogram
@@ -777,6 +788,7 @@ __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_
   __shared__ uint32_t tile_lo[2];  // C16: low byte of the tile's first, last record
 
   const int t = threadIdx.x;
+  const bool bkt = BLOCK == kBuckets || t < kBuckets;  // a bucket thread
   const int w = t >> 6;
   const uint32_t lane = lane_id();
   const int64_t TT = (m + T - 1) / T;
@@ -799,13 +811,13 @@ __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_
   uint64_t tot = 0;
 #pragma unroll
   for (int x = 0; x < kSub; ++x) {
-    const uint32_t v = sub_hist[x * kBuckets + t];
+    const uint32_t v = bkt ? sub_hist[x * kBuckets + t] : 0u;
     if (HALVES == 1) col[x] = v;
     tot += v;
   }
   uint64_t all;
   const uint64_t bstart = block_exclusive_scan<BLOCK>(tot, scan64, &all);
-  if (totals != nullptr && blockIdx.x == 0) totals[t] = tot;
+  if (totals != nullptr && blockIdx.x == 0 && bkt) totals[t] = tot;
   // Skewed digit (one bucket holds more than 1/32 of the records, e.g. Zipf
   // keys): runs of equal next digits are then long, and 64 lanes adding to
   // one LDS counter serialise.  Such launches add once per run of equal
@@ -864,7 +876,7 @@ __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_
       uint64_t pre = 0;
 #pragma unroll
       for (int xx = 0; xx < kSub; ++xx)
-        pre += xx < x ? (HALVES == 1 ? col[xx] : sub_hist[xx * kBuckets + t]) : 0u;
+        pre += xx < x ? (HALVES == 1 ? col[xx] : (bkt ? sub_hist[xx * kBuckets + t] : 0u)) : 0u;
       base = bstart + pre;
     }
     const int64_t tb = (int64_t)tile * T;
@@ -917,7 +929,7 @@ __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_
       const uint32_t below = mbcnt(mt);
       const uint32_t pre = wcnt[w][d];
       rk[i] = pre + below;
-      if (valid && below == 0) wcnt[w][d] = pre + (uint32_t)__popcll(mt);
+      if (valid && below == 0) wcnt[w][d] = (WC)(pre + (uint32_t)__popcll(mt));
       if (C16) {
         const int li = wbase + i * 64;
         if (li == 0) tile_lo[0] = (uint32_t)(e[i].key >> shift16) & 0xFFu;
@@ -926,11 +938,13 @@ __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_
     }
     __syncthreads();
     OS_MARK(1);  // load + rank
+    if (bkt) {
 #pragma unroll
-    for (int ww = 0; ww < W; ++ww) {
-      const uint32_t v = wcnt[ww][t];
-      wcnt[ww][t] = cnt;
-      cnt += v;
+      for (int ww = 0; ww < W; ++ww) {
+        const uint32_t v = wcnt[ww][t];
+        wcnt[ww][t] = (WC)cnt;
+        cnt += v;
+      }
     }
     bool mixed16 = false;
     if (C16) {
@@ -945,7 +959,7 @@ __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_
       }
     }
     const uint32_t cnt_b = pair_swap(cnt);  // even lanes: lane t + 1's count
-    if (even) {
+    if (even && bkt) {
       const uint32_t tg = head ? tag_pre : tag_agg;
       __builtin_amdgcn_raw_buffer_store_b64(v2u{cnt | tg, cnt_b | tg}, rs, my_off, 0, kStPol);
       if (!head) load_window();
@@ -953,8 +967,10 @@ __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_
     {
       uint32_t tile_total;
       lstart = block_exclusive_scan<BLOCK>(cnt, scan32, &tile_total);
+      if (bkt) {
 #pragma unroll
-      for (int ww = 0; ww < W; ++ww) wcnt[ww][t] += lstart;
+        for (int ww = 0; ww < W; ++ww) wcnt[ww][t] = (WC)(wcnt[ww][t] + lstart);
+      }
     }
     __syncthreads();
     OS_MARK(2);  // publish + scan
@@ -978,7 +994,7 @@ __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_
 
     OS_MARK(3);  // stage
     uint32_t ea = 0, eb = 0;
-    if (even && !head) {
+    if (even && bkt && !head) {
       uint32_t spins = 0;
       for (;;) {
         // Rows in order, while they are ready: both halves of this launch
@@ -1017,8 +1033,8 @@ __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_
     const uint32_t eb_left = pair_swap(eb);  // odd lanes: lane t - 1's sum
     const uint64_t excl = even ? ea : eb_left;
     const int64_t R = (int64_t)(base + excl);  // first output slot of the run
-    delta[t] = R - (int64_t)lstart;
-    if (NEXT) {
+    if (bkt) delta[t] = R - (int64_t)lstart;
+    if (NEXT && bkt) {
       // The run [R, R + cnt) lies in next-pass sub-array x0, except from
       // stage position jb on (x1) when it crosses a sub-array boundary (at
       // most one: a non-empty sub-array holds >= kTile records).
@@ -1663,7 +1679,7 @@ hipError_t launch_onesweep(const Elem* in, Elem* out, int64_t m, int shift, int 
   int64_t g = split ? (int64_t)grid * 3 / 2 : grid;
   if (g < kSub) g = kSub;
   if (g > (TT + kSub - 1) / kSub * kSub) g = (TT + kSub - 1) / kSub * kSub;
-  const dim3 gd((unsigned)g), bd(kScatterBlock);
+  const dim3 gd((unsigned)g), bd(split ? kOsSplitBlock : kOsBlock);
   uint32_t* st = status;
   if (c16) {
     // The 16-bit counts need the low byte below this digit, and no next
@@ -1671,24 +1687,24 @@ hipError_t launch_onesweep(const Elem* in, Elem* out, int64_t m, int shift, int 
     if (shift < 8 || next_shift >= 0) return hipErrorInvalidValue;
     e = hipMemsetAsync(c16, 0, sizeof(uint64_t) * 65536, s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_onesweep<kScatterBlock, kScatterIpt, false, true, 1>), gd, bd, 0, s, in, out,
+    hipLaunchKernelGGL((k_onesweep<kOsBlock, kOsIpt, false, true, 1>), gd, bd, 0, s, in, out,
                        m, shift, 0, sub_hist, nullptr, st, tile_ctr, epoch, err, extra.totals, c16);
   } else if (next_shift >= 0) {
     e = hipMemsetAsync(next_hist, 0, sizeof(uint32_t) * kSub * kBuckets, s);
     if (e != hipSuccess) return e;
     if (split)
-      hipLaunchKernelGGL((k_onesweep<kScatterBlock, kScatterIpt, true, false, 2>), gd, bd, 0, s, in, out,
+      hipLaunchKernelGGL((k_onesweep<kOsSplitBlock, kOsSplitIpt, true, false, 2>), gd, bd, 0, s, in, out,
                          m, shift, next_shift, sub_hist, next_hist, st, tile_ctr, epoch, err,
                          extra.totals, nullptr);
     else
-      hipLaunchKernelGGL((k_onesweep<kScatterBlock, kScatterIpt, true, false, 1>), gd, bd, 0, s, in, out,
+      hipLaunchKernelGGL((k_onesweep<kOsBlock, kOsIpt, true, false, 1>), gd, bd, 0, s, in, out,
                          m, shift, next_shift, sub_hist, next_hist, st, tile_ctr, epoch, err,
                          extra.totals, nullptr);
   } else if (split) {
-    hipLaunchKernelGGL((k_onesweep<kScatterBlock, kScatterIpt, false, false, 2>), gd, bd, 0, s, in, out,
+    hipLaunchKernelGGL((k_onesweep<kOsSplitBlock, kOsSplitIpt, false, false, 2>), gd, bd, 0, s, in, out,
                        m, shift, 0, sub_hist, nullptr, st, tile_ctr, epoch, err, extra.totals, nullptr);
   } else {
-    hipLaunchKernelGGL((k_onesweep<kScatterBlock, kScatterIpt, false, false, 1>), gd, bd, 0, s, in, out,
+    hipLaunchKernelGGL((k_onesweep<kOsBlock, kOsIpt, false, false, 1>), gd, bd, 0, s, in, out,
                        m, shift, 0, sub_hist, nullptr, st, tile_ctr, epoch, err, extra.totals, nullptr);
   }
   return hipGetLastError();

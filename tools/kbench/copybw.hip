@@ -101,6 +101,48 @@ __global__ void k_copyT(const ulonglong2* __restrict__ a, ulonglong2* __restrict
   }
 }
 
+// The same tile copy with BLOCK threads per workgroup (tile = BLOCK * IPT
+// records), optional streaming (nontemporal) loads, and PF = 1: the next
+// tile's loads are issued before this tile's stores (software pipeline,
+// twice the registers).
+template <int BLOCK, int IPT, bool NT, bool PF>
+__global__ __launch_bounds__(BLOCK) void k_copyTB(const ulonglong2* __restrict__ a, ulonglong2* __restrict__ o,
+                                                  int64_t n) {
+  constexpr int T = BLOCK * IPT;
+  __shared__ ulonglong2 st[T];
+  const int64_t tiles = n / T;
+  typedef unsigned long long v2u64 __attribute__((ext_vector_type(2)));
+  auto ld = [&](int64_t i) -> ulonglong2 {
+    if (NT) {
+      const v2u64 x = __builtin_nontemporal_load(reinterpret_cast<const v2u64*>(a + i));
+      return make_ulonglong2(x.x, x.y);
+    }
+    return a[i];
+  };
+  ulonglong2 v[IPT];
+  int64_t tile = blockIdx.x;
+  if (PF && tile < tiles) {
+#pragma unroll
+    for (int u = 0; u < IPT; ++u) v[u] = ld(tile * T + u * BLOCK + threadIdx.x);
+  }
+  for (; tile < tiles; tile += gridDim.x) {
+    if (!PF) {
+#pragma unroll
+      for (int u = 0; u < IPT; ++u) v[u] = ld(tile * T + u * BLOCK + threadIdx.x);
+    }
+#pragma unroll
+    for (int u = 0; u < IPT; ++u) st[u * BLOCK + threadIdx.x] = v[u];
+    __syncthreads();
+    if (PF && tile + gridDim.x < tiles) {
+#pragma unroll
+      for (int u = 0; u < IPT; ++u) v[u] = ld((tile + gridDim.x) * T + u * BLOCK + threadIdx.x);
+    }
+#pragma unroll
+    for (int u = 0; u < IPT; ++u) o[tile * T + u * BLOCK + threadIdx.x] = st[u * BLOCK + threadIdx.x];
+    __syncthreads();
+  }
+}
+
 __global__ void k_read(const ulonglong2* __restrict__ a, int64_t n, unsigned long long* sink) {
   const int64_t i0 = (int64_t)blockIdx.x * blockDim.x * 4 + threadIdx.x;
   uint64_t s = 0;
@@ -169,6 +211,16 @@ int main(int argc, char** argv) {
     snprintf(nm, sizeof nm, "copyT8 g%d", g);
     rep(nm, time_ms([&] { k_copyT<8><<<g, 256>>>(a, o, n); }, reps), cp);
   }
+  // Shape study for k_onesweep (4096-record tiles, 64 KiB of LDS, 2 per CU):
+  // waves per workgroup, streaming loads, next-tile prefetch.
+  rep("TB256x16 g512", time_ms([&] { k_copyTB<256, 16, false, false><<<512, 256>>>(a, o, n); }, reps), cp);
+  rep("TB256x16nt g512", time_ms([&] { k_copyTB<256, 16, true, false><<<512, 256>>>(a, o, n); }, reps), cp);
+  rep("TB512x8 g512", time_ms([&] { k_copyTB<512, 8, false, false><<<512, 512>>>(a, o, n); }, reps), cp);
+  rep("TB512x8nt g512", time_ms([&] { k_copyTB<512, 8, true, false><<<512, 512>>>(a, o, n); }, reps), cp);
+  rep("TB1024x4 g512", time_ms([&] { k_copyTB<1024, 4, false, false><<<512, 1024>>>(a, o, n); }, reps), cp);
+  rep("TB256x16pf g512", time_ms([&] { k_copyTB<256, 16, false, true><<<512, 256>>>(a, o, n); }, reps), cp);
+  rep("TB512x8pf g512", time_ms([&] { k_copyTB<512, 8, false, true><<<512, 512>>>(a, o, n); }, reps), cp);
+  rep("TB256x12 g512", time_ms([&] { k_copyTB<256, 12, false, false><<<512, 256>>>(a, o, n); }, reps), cp);
   rep("read4", time_ms([&] { k_read<<<(n + 1023) / 1024, 256>>>(a, n, sink); }, reps), one);
   rep("write4", time_ms([&] { k_write<<<(n + 1023) / 1024, 256>>>(o, n); }, reps), one);
   rep("hipMemcpyD2D", time_ms([&] { CK(hipMemcpyAsync(o, a, n * 16, hipMemcpyDeviceToDevice, 0)); }, reps), cp);
