@@ -30,7 +30,10 @@ constexpr int kTile = kScatterBlock * kScatterIpt;  // 4096 elements = 64 KiB in
 // 4 waves x 16 for the split stage (3 per CU; at 8 waves its registers spill).
 constexpr int kOsBlock = LSB_OS_BLOCK;
 constexpr int kOsIpt = kTile / kOsBlock;
-constexpr int kOsSplitBlock = 256;
+#ifndef LSB_OS_SPLIT_BLOCK
+#define LSB_OS_SPLIT_BLOCK 256
+#endif
+constexpr int kOsSplitBlock = LSB_OS_SPLIT_BLOCK;
 constexpr int kOsSplitIpt = kTile / kOsSplitBlock;
 static_assert(kOsBlock % kBuckets == 0 && kOsBlock * kOsIpt == kTile, "onesweep tile shape");
 constexpr int kMaxChunks = 65536;             // upper bound on the chunk grid
