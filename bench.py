@@ -360,7 +360,9 @@ def make_world(a, d, N, n_total, radix):
         w = lsbsort.World.rank_ops(n_total, N, d.rank, device, GlooComm(d.dist, d.world, d.rank),
                                    radix_bits=radix)
     elif d.world > 1:
-        device = d.local_rank
+        # One GPU per rank; the modulo keeps a launcher that narrows each
+        # rank's visible devices (HIP_VISIBLE_DEVICES) on that rank's GPU.
+        device = d.local_rank % max(1, visible_devices())
         if a.transport == "rccl-sockets":
             # Ranks may share a GPU: RCCL accepts that only across "hosts",
             # so each rank is its own host and the wire is a loopback socket.
