@@ -16,6 +16,13 @@ the max over ranks.  The result of the last step is verified on device
 Multi-GPU: one process per GPU (RANK / WORLD_SIZE / LOCAL_RANK from the
 environment).  torch.distributed (gloo, CPU) only ships the RCCL unique id
 and reduces timings; the data path is the library's own RCCL communicator.
+`python bench.py --gpus N` with no launcher starts the N rank processes
+itself (the way `mpirun -n N` starts the reference's ranks,
+mpi/README.md:24-28): this parent never touches HIP; it relays rank 0's line
+and fails with the failing rank's stderr tail.  Under torch.distributed.run
+the ranks are the launcher's processes.  Either way the whole-key extra runs
+in fresh rank processes of its own after the headline is measured, so a
+failure there costs only its own keys.
 At N > 1 the headline is the reference's own structure (BASELINE configs[2],
 configs[3]): per 16-bit digit (the reference's RADIX 16) an RCCL AllGather
 of the counts and an RCCL AllToAllv of the records (--radix-bits 16;
@@ -66,6 +73,11 @@ def parse():
     ap.add_argument("--no-whole-key", action="store_true",
                     help="N > 1: skip the extra whole-key exchange timing")
     ap.add_argument("--probe", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--dry-rank", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--dry-fail", type=int, default=-1, help=argparse.SUPPRESS)
+    ap.add_argument("--dry-fail-whole-key", type=int, default=-1, help=argparse.SUPPRESS)
+    ap.add_argument("--rank-timeout", type=int, default=1500,
+                    help="self-launched rank processes: seconds before they are stopped")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--radix-bits", type=int, default=0, choices=(0, 8, 16, 64),
                     help="exchange digit width: 8 or 16 (one all-to-all per digit), or 64 (the "
@@ -416,6 +428,166 @@ def timed_sorts(w, d, a, steps, warmup):
     return d.max(sum(times)), verified, d.max_list(times)
 
 
+def free_port():
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def rank_env(rank, world, local_rank, port, master="127.0.0.1"):
+    """Environment of one rank process, as torch.distributed.run sets it.  A
+    launcher's own agent-store variables are dropped: the child forms a new
+    group on its own port (TORCHELASTIC_USE_AGENT_STORE would make every
+    child a client of a store nobody serves)."""
+    env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC_")}
+    env.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(local_rank),
+               LOCAL_WORLD_SIZE=str(world), MASTER_ADDR=master, MASTER_PORT=str(port))
+    return env
+
+
+def spawn_ranks(argv, ranks, timeout, label):
+    """Run this script once per (rank, env) in `ranks` as fresh processes and
+    wait.  Returns (ok, stdout of the first process, failure report).  When a
+    process fails, the others get 60 s (they may be waiting in a collective
+    the failed rank never joins) and are then stopped."""
+    import tempfile
+    tmp = tempfile.mkdtemp(prefix="lsb-bench-")
+    procs = []
+    for i, env in enumerate(ranks):
+        out = open(os.path.join(tmp, f"{i}.out"), "w+")
+        err = open(os.path.join(tmp, f"{i}.err"), "w+")
+        p = subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + argv, env=env,
+                             stdout=out, stderr=err, start_new_session=True)
+        procs.append((p, out, err))
+    t0 = time.time()
+    first_fail = None
+    beat = t0
+    while any(p.poll() is None for p, _, _ in procs):
+        time.sleep(0.5)
+        now = time.time()
+        if first_fail is None and any(p.poll() not in (None, 0) for p, _, _ in procs):
+            first_fail = now
+        late = (first_fail is not None and now - first_fail > 60) or now - t0 > timeout
+        if late:
+            for p, _, _ in procs:
+                if p.poll() is None:
+                    try:
+                        os.killpg(p.pid, 9)  # the process group this call started
+                    except OSError:
+                        pass
+            for p, _, _ in procs:
+                p.wait()
+            break
+        if now - beat > 30:
+            beat = now
+            print(f"[bench] {label}: {len(procs)} rank processes running, {now - t0:.0f} s",
+                  file=sys.stderr, flush=True)
+    codes = [p.returncode for p, _, _ in procs]
+    texts = []
+    for _, out, err in procs:
+        out.seek(0)
+        err.seek(0)
+        texts.append((out.read(), err.read()))
+        out.close()
+        err.close()
+    shutil.rmtree(tmp, ignore_errors=True)
+    ok = all(c == 0 for c in codes)
+    report = ""
+    if not ok:
+        bad = [i for i, c in enumerate(codes) if c != 0]
+        report = f"{label}: rank exit codes {codes}; " + " | ".join(
+            f"rank {i} stderr tail: {texts[i][1][-1500:]}" for i in bad[:2])
+    return ok, texts[0][0], report
+
+
+def last_json(text):
+    lines = [l for l in text.splitlines() if l.startswith("{")]
+    return json.loads(lines[-1]) if lines else None
+
+
+def whole_key_argv(a):
+    """The command line of the whole-key extra: this run's flags with the
+    64-bit exchange digit, fewer steps, no extras of its own."""
+    argv = sys.argv[1:] + ["--radix-bits", "64", "--steps", str(min(a.steps, 3)), "--warmup", "1",
+                           "--no-cpu-baseline", "--no-whole-key", "--no-traffic"]
+    if a.exchange == "peer":  # a per-digit form; the whole key goes by AllToAllv
+        argv += ["--exchange", "alltoallv"]
+    return argv
+
+
+def merge_whole_key(out, ok, text, report):
+    """The extra's keys into the headline line."""
+    r = last_json(text) if ok else None
+    if r is None:
+        out["whole_key_error"] = report or "no result line"
+        return
+    out["whole_key_melem_s"] = r["value"]
+    out["whole_key_ms_per_step"] = r["ms_per_step"]
+    out["whole_key_verified"] = r["verified"]
+
+
+def rank_whole_key(a, d, out):
+    """Launcher-started ranks (torch.distributed.run): the whole-key exchange
+    (one all-to-all per sort), same input, fewer steps, in one fresh process
+    per rank (this rank's context is closed by now), so a failure there costs
+    only its own keys.  Every rank takes the same branch: the children's
+    success is agreed on before rank 0 reads its child's line."""
+    port = d.bcast_bytes(free_port() if d.rank == 0 else None)
+    env = rank_env(d.rank, d.world, d.local_rank, port, os.environ.get("MASTER_ADDR", "127.0.0.1"))
+    ok, text, report = spawn_ranks(whole_key_argv(a), [env], a.rank_timeout, "whole-key extra")
+    ok = d.all_true(ok)
+    if d.rank == 0:
+        merge_whole_key(out, ok, text, report or ("" if ok else "another rank's process failed"))
+
+
+def dry_run(a):
+    """--dry-rank (tests, CPU): the launch plumbing without a GPU.  Each rank
+    joins the gloo group and max-reduces its rank; rank 0 prints a line of
+    the bench's shape; --dry-fail R makes rank R exit with status 3 (and
+    --dry-fail-whole-key R rank R of the whole-key extra)."""
+    d = Dist()
+    radix = a.radix_bits or (8 if d.world == 1 else 16)
+    if d.rank == (a.dry_fail_whole_key if radix == 64 else a.dry_fail):
+        sys.exit(3)
+    top = d.max(float(d.rank))
+    out = {"metric": METRIC, "value": float(d.world * radix), "ms_per_step": 1.0, "verified": True,
+           "n_gpus": d.world, "max_rank": top, "radix_bits": radix,
+           "config": {"n_total": a.n_per_gpu * d.world}}
+    if d.world > 1 and radix != 64 and not a.no_whole_key:
+        rank_whole_key(a, d, out)
+    d.barrier()
+    d.close()
+    if d.rank == 0:
+        print(json.dumps(out), flush=True)
+
+
+def launch(a):
+    """`bench.py --gpus N` without a launcher: start the N rank processes
+    here (one per GPU, RANK / WORLD_SIZE / LOCAL_RANK / MASTER_* set as
+    torch.distributed.run would), relay rank 0's line.  Nothing in this
+    process initialises HIP."""
+    N = a.gpus
+    argv = sys.argv[1:] + ["--no-cpu-baseline", "--no-whole-key"]
+    port = free_port()
+    ok, text, report = spawn_ranks(argv, [rank_env(r, N, r, port) for r in range(N)], a.rank_timeout,
+                                   "headline")
+    out = last_json(text) if ok else None
+    if out is None:
+        print(f"bench.py: {report or 'rank 0 printed no result line'}", file=sys.stderr, flush=True)
+        sys.exit(1)
+    out["launcher"] = f"bench.py started {N} rank processes (one per GPU)"
+    radix = a.radix_bits or 16
+    if radix != 64 and not a.no_whole_key:
+        port = free_port()
+        merge_whole_key(out, *spawn_ranks(whole_key_argv(a), [rank_env(r, N, r, port) for r in range(N)],
+                                          a.rank_timeout, "whole-key extra"))
+    out["cpu_baseline"] = None if a.no_cpu_baseline else cpu_baseline(out["config"]["n_total"], a.cpu_n)
+    print(json.dumps(out), flush=True)
+    if out.get("verified") is False or out.get("whole_key_verified") is False:
+        sys.exit(1)
+
+
 def probe(a):
     """One sort of the workload, nothing printed: the program rocprofv3's
     --pmc passes run (measure_traffic)."""
@@ -427,10 +599,36 @@ def probe(a):
     w.close()
 
 
+def per_pass_rows(passes, steps, kernel, N):
+    """Per local pass, per step (lsb_get_pass_stats): the scatter kernel's
+    time, its HBM rate (32 algorithmic bytes per record) and its fraction of
+    the peak, plus the pass's count, exchange and placement time."""
+    rows = []
+    for p in passes:
+        if not p["launches"]:
+            continue
+        avg = p["ms_scatter"] / p["launches"]
+        gbs = SCATTER_BYTES_PER_ELEM * (p["elems"] / p["launches"]) / (avg / 1e3) / 1e9 if avg > 0 else 0.0
+        row = {"pass": p["pass"], "shift": p["shift"], "kernel": kernel,
+               "ms": round(p["ms_scatter"] / steps, 4), "gbs": round(gbs, 1),
+               "frac": round(gbs / HBM_PEAK_GBS, 4)}
+        if p["ms_count"]:
+            row["count_ms"] = round(p["ms_count"] / steps, 4)
+        if N > 1 or p["ms_exchange"] or p["ms_place"]:
+            row["exchange_ms"] = round(p["ms_exchange"] / steps, 4)
+            row["place_ms"] = round(p["ms_place"] / steps, 4)
+        rows.append(row)
+    return rows
+
+
 def main():
     a = parse()
     if a.probe:
         return probe(a)
+    if a.gpus > 1 and int(os.environ.get("WORLD_SIZE", "1")) <= 1:
+        return launch(a)
+    if a.dry_rank:
+        return dry_run(a)
     d = Dist()
     N = d.world if d.world > 1 else a.gpus
     n_total = a.n_per_gpu * N
@@ -446,6 +644,7 @@ def main():
 
     total, verified, step_s = timed_sorts(w, d, a, a.steps, a.warmup)
     stats = w.kernel_stats()
+    passes = w.pass_stats()
     scatter_elems = w.scatter_elems()
     xcalls, xbytes, _ = w.exchange_bytes()
     last = w.last_sort()
@@ -531,6 +730,7 @@ def main():
                             "basis": "SURVEY.md 8(d): 48*D*n / (t_sort * P * 8e12), fixed denominator, "
                                      "median step"},
         "kernel_ms_per_step": {k: round(v[1] / a.steps, 3) for k, v in stats.items()},
+        "per_pass": per_pass_rows(passes, a.steps, kernel, N),
         "kernel_ms_per_step_legend": {
             "upsweep": "count read (k_subhist once per sort, or k_upsweep per pass)",
             "scan": "chunk scan (k_scan, reduce-then-scan only)",
@@ -545,19 +745,7 @@ def main():
         "library": lsbsort.build_info(),
     }
     if N > 1 and radix != 64 and not a.no_whole_key:
-        # The whole-key exchange (one all-to-all per sort), same input, fewer
-        # steps.  An extra key: a library error here must not cost the
-        # headline line.
-        try:
-            wk, _ = make_world(a, d, N, n_total, 64)
-            k = min(a.steps, 3)
-            wt, wv, _ = timed_sorts(wk, d, a, k, 1)
-            wk.close()
-            out["whole_key_melem_s"] = round(n_total * k / wt / 1e6, 2)
-            out["whole_key_ms_per_step"] = round(wt / k * 1e3, 3)
-            out["whole_key_verified"] = wv
-        except lsbsort.LsbError as e:
-            out["whole_key_error"] = str(e)
+        rank_whole_key(a, d, out)
     if d.rank == 0 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(n_total, a.cpu_n)
     elif d.rank == 0:

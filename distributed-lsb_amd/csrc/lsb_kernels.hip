@@ -1655,7 +1655,9 @@ int onesweep_halves_for(const uint32_t* h, int64_t m) {
   for (int b = 0; b < kBuckets; ++b) {
     uint64_t tot = 0;
     for (int x = 0; x < kSub; ++x) tot += h[x * kBuckets + b];
-    if (tot > (uint64_t)(m >> 5)) return 2;  // the kernel's own `skewed` test
+    // The kernel's own `skewed` test; a bucket holding every record is a
+    // constant byte of this rank (its pass is the identity), not skew.
+    if (tot > (uint64_t)(m >> 5) && tot < (uint64_t)m) return 2;
   }
   return 1;
 }

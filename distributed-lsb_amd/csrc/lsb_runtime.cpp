@@ -49,6 +49,7 @@ enum class Mode { kLoopback, kRccl, kOps };
 struct PendingEvent {
   int kid;
   int dev;
+  int pass;  // local pass the launch is filed under (lsb_get_pass_stats), -1: none
   hipEvent_t start, stop;
 };
 
@@ -95,6 +96,7 @@ struct Rank {
   uint32_t* os_hist_h = nullptr;        // pinned mirror of a sub-array histogram
   int os_halves = 1;                    // this sort's k_onesweep stage split (1 or 2)
   uint32_t os_epoch = 0;                // last look-back epoch
+  bool os_dirty = false;                // a launch failed: zero os_status before the next
   int os_grid = 0;                      // persistent grid (2 workgroups per CU)
   // Per-digit exchange with single-read local passes (sort_exchange_onesweep):
   // os_hist[os_cur] is A's sub-array histogram of the byte at os_valid (-1:
@@ -153,6 +155,14 @@ struct lsb_ctx {
   int64_t launches[LSB_K_COUNT] = {};
   double total_ms[LSB_K_COUNT] = {};
   int64_t scatter_elems = 0;
+  // Per local pass (lsb_get_pass_stats): the pass the next timed launch is
+  // filed under (pass_cursor counts the local passes of the current sort).
+  int cur_pass = 0;
+  int pass_cursor = 0;
+  int pass_shift[LSB_MAX_PASSES] = {};
+  int64_t pass_launches[LSB_MAX_PASSES][LSB_K_COUNT] = {};
+  double pass_ms[LSB_MAX_PASSES][LSB_K_COUNT] = {};
+  int64_t pass_elems[LSB_MAX_PASSES] = {};
 };
 
 namespace {
@@ -212,10 +222,12 @@ struct Timer {
   lsb_ctx* c;
   Rank* r;
   int kid;
+  int pass;
   hipStream_t stream;
   hipEvent_t start = nullptr;
   Timer(lsb_ctx* c_, Rank* r_, int kid_, hipStream_t s = nullptr)
-      : c(c_), r(r_), kid(kid_), stream(s ? s : r_->stream) {
+      : c(c_), r(r_), kid(kid_), pass(kid_ == LSB_K_SORT ? -1 : c_->cur_pass),
+        stream(s ? s : r_->stream) {
     if (!c->timing) return;
     start = take_event(c);
     if (start) (void)hipEventRecord(start, stream);
@@ -225,11 +237,25 @@ struct Timer {
     hipEvent_t e = take_event(c);
     if (!e) return;
     (void)hipEventRecord(e, stream);
-    c->pending.push_back({kid, r->dev, start, e});
+    c->pending.push_back({kid, r->dev, pass, start, e});
     start = nullptr;
   }
   ~Timer() { stop(); }
 };
+
+// The local pass the following launches belong to: the pass_cursor-th local
+// pass of this sort, on the byte at `shift` (lsb_get_pass_stats).
+void begin_pass(lsb_ctx* c, int shift) {
+  c->cur_pass = c->pass_cursor++;
+  if (c->cur_pass < LSB_MAX_PASSES) c->pass_shift[c->cur_pass] = shift;
+}
+
+// Records one local pass of m records processed (the scatter kernel's elements).
+void count_pass_elems(lsb_ctx* c, int64_t m) {
+  if (!c->timing) return;
+  c->scatter_elems += m;
+  if (c->cur_pass >= 0 && c->cur_pass < LSB_MAX_PASSES) c->pass_elems[c->cur_pass] += m;
+}
 
 int resolve_timing(lsb_ctx* c) {
   for (auto& p : c->pending) {
@@ -239,6 +265,10 @@ int resolve_timing(lsb_ctx* c) {
     HIP_TRY(hipEventElapsedTime(&ms, p.start, p.stop));
     c->launches[p.kid] += 1;
     c->total_ms[p.kid] += ms;
+    if (p.pass >= 0 && p.pass < LSB_MAX_PASSES) {
+      c->pass_launches[p.pass][p.kid] += 1;
+      c->pass_ms[p.pass][p.kid] += ms;
+    }
     c->event_pool.push_back(p.start);
     c->event_pool.push_back(p.stop);
   }
@@ -395,7 +425,7 @@ int local_pass(lsb_ctx* c, Rank& r, int shift, bool want_span = false, bool star
     Timer t(c, &r, LSB_K_SCATTER);
     HIP_TRY(lsb::launch_scatter(r.A, r.B, r.here, shift, ch, r.chunk_off, r.totals,
                                 starts16 ? r.first16 : nullptr, r.stream));
-    if (c->timing) c->scatter_elems += r.here;
+    count_pass_elems(c, r.here);
   }
   std::swap(r.A, r.B);
   return LSB_OK;
@@ -851,6 +881,7 @@ int do_pass(lsb_ctx* c, int digit, uint64_t varying = ~0ull, bool want_span = fa
     if (!want_span && ((varying >> shift) & (lsb::kBuckets - 1)) == 0) continue;
     // The high byte of a 16-bit exchange digit also marks the digit's starts.
     const bool starts16 = exchanging(c) && subs == 2 && sub == 1;
+    begin_pass(c, shift);
     for (Rank& r : c->ranks) LSB_TRY(local_pass(c, r, shift, want_span && sub == 0, starts16));
     ++c->last_local_passes;
   }
@@ -887,11 +918,38 @@ int onesweep_ensure(Rank& r) {
   return LSB_OK;
 }
 
-// A fresh look-back epoch for the next k_onesweep launch of rank r.
-// Granules carry the epoch's parity, and every launch rewrites every row, so
-// only the alternation matters (the counter runs on for the record).
-int next_epoch(Rank& r) {
-  if (++r.os_epoch >= (1u << 30)) r.os_epoch = 2;  // 2^30 is even: keep the alternation
+// One k_onesweep launch of rank r, r.A -> r.B on the byte at `shift` (then
+// the buffers swap), under a fresh look-back epoch.  Granules carry the
+// epoch's parity, and every launch rewrites every row, so only the
+// alternation matters (the counter runs on for the record).  The epoch
+// advances only once the launch is queued: a launch that fails before its
+// kernel runs writes no rows, and a later launch would then accept rows of
+// two launches back as current.  So a failure marks the rows dirty; the next
+// launch zeroes them first and restarts the epochs (the first is odd).
+int onesweep_launch(lsb_ctx* c, Rank& r, int shift, int next, const uint32_t* hist,
+                    uint32_t* next_hist, lsb::OnesweepExtra x) {
+  const size_t status_bytes = (size_t)lsb::onesweep_tiles(r.here) * lsb::kBuckets * sizeof(uint32_t);
+  if (r.os_dirty) {
+    HIP_TRY(hipMemsetAsync(r.os_status, 0, status_bytes, r.stream));
+    r.os_epoch = 0;
+    r.os_dirty = false;
+  }
+  uint32_t epoch = r.os_epoch + 1;
+  if (epoch >= (1u << 30)) epoch = 2;  // 2^30 is even: keep the alternation
+  hipError_t e;
+  {
+    Timer t(c, &r, LSB_K_SCATTER);
+    e = lsb::launch_onesweep(r.A, r.B, r.here, shift, next, hist, next_hist, r.os_status, r.os_ctr,
+                             epoch, r.os_ctr + lsb::kOnesweepSubs, r.os_grid, r.stream, x);
+  }
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    r.os_dirty = true;
+    return fail(LSB_ERR_HIP, "launch_onesweep", hipGetErrorString(e));
+  }
+  r.os_epoch = epoch;
+  count_pass_elems(c, r.here);
+  std::swap(r.A, r.B);
   return LSB_OK;
 }
 
@@ -919,12 +977,17 @@ int choose_halves(lsb_ctx* c, Rank& r, bool synced) {
 // lsb_sort when nothing is exchanged: one k_subhist read (digit 0's
 // sub-array histogram and the key span), then one k_onesweep per digit that
 // varies, each also counting the next such digit over its output.  Same
-// passes, same output as the reduce-then-scan loop (do_pass).
+// output as the reduce-then-scan loop (do_pass).  A constant digit 0 is
+// skipped like any other: its pass would be the identity, so the first
+// digit that varies is counted by a second k_subhist read (a read, not a
+// pass), and that digit's histogram also decides the stage split.
 // Rank r alone (its local block); *passes gets the passes it ran, *varying the
 // key bits that vary in the block.
 int sort_onesweep_rank(lsb_ctx* c, Rank& r, int* passes, uint64_t* varying) {
   HIP_TRY(hipSetDevice(r.dev));
   LSB_TRY(onesweep_ensure(r));
+  c->pass_cursor = 0;
+  c->cur_pass = 0;  // the count reads are filed under the first pass
   const int64_t m = r.here;
   uint32_t* hist[2] = {r.os_hist, r.os_hist + lsb::kOnesweepSubs * lsb::kBuckets};
   HIP_TRY(hipMemsetAsync(r.span, 0, 2 * sizeof(uint64_t), r.stream));
@@ -934,7 +997,6 @@ int sort_onesweep_rank(lsb_ctx* c, Rank& r, int* passes, uint64_t* varying) {
                                 r.stream));
   }
   LSB_TRY(queue_halves(c, r, hist[0]));
-  std::vector<int> digits{0};
   *varying = ~0ull;
   *passes = 0;
   if (c->skip_constant) {
@@ -942,23 +1004,26 @@ int sort_onesweep_rank(lsb_ctx* c, Rank& r, int* passes, uint64_t* varying) {
     HIP_TRY(hipStreamSynchronize(r.stream));
     *varying = r.span_h[0] & r.span_h[1];
   }
-  LSB_TRY(choose_halves(c, r, c->skip_constant));
-  for (int d = 1; d < 64 / lsb::kDigitBits; ++d)
+  std::vector<int> digits;
+  for (int d = 0; d < 64 / lsb::kDigitBits; ++d)
     if (((*varying >> (d * lsb::kDigitBits)) & (lsb::kBuckets - 1)) != 0) digits.push_back(d);
+  if (!digits.empty() && digits[0] != 0) {
+    Timer t(c, &r, LSB_K_UPSWEEP);
+    HIP_TRY(lsb::launch_subhist(r.A, m, digits[0] * lsb::kDigitBits, r.os_grid, hist[0], nullptr,
+                                r.stream));
+    t.stop();
+    LSB_TRY(queue_halves(c, r, hist[0]));
+    LSB_TRY(choose_halves(c, r, false));
+  } else {
+    LSB_TRY(choose_halves(c, r, c->skip_constant));
+  }
   for (size_t i = 0; i < digits.size(); ++i) {
     const int shift = digits[i] * lsb::kDigitBits;
     const int next = i + 1 < digits.size() ? digits[i + 1] * lsb::kDigitBits : -1;
-    LSB_TRY(next_epoch(r));
-    {
-      Timer t(c, &r, LSB_K_SCATTER);
-      lsb::OnesweepExtra x;
-      x.halves = r.os_halves;
-      HIP_TRY(lsb::launch_onesweep(r.A, r.B, m, shift, next, hist[i & 1], hist[(i + 1) & 1],
-                                   r.os_status, r.os_ctr, r.os_epoch,
-                                   r.os_ctr + lsb::kOnesweepSubs, r.os_grid, r.stream, x));
-      if (c->timing) c->scatter_elems += m;
-    }
-    std::swap(r.A, r.B);
+    begin_pass(c, shift);
+    lsb::OnesweepExtra x;
+    x.halves = r.os_halves;
+    LSB_TRY(onesweep_launch(c, r, shift, next, hist[i & 1], hist[(i + 1) & 1], x));
     ++*passes;
   }
   // The look-back's give-up word, read by lsb_sync.
@@ -1006,15 +1071,7 @@ int local_pass_os(lsb_ctx* c, Rank& r, int shift, int next, lsb::OnesweepExtra e
     Timer t(c, &r, LSB_K_UPSWEEP);
     HIP_TRY(lsb::launch_subhist(r.A, m, shift, r.os_grid, hist[r.os_cur], nullptr, r.stream));
   }
-  LSB_TRY(next_epoch(r));
-  {
-    Timer t(c, &r, LSB_K_SCATTER);
-    HIP_TRY(lsb::launch_onesweep(r.A, r.B, m, shift, next, hist[r.os_cur], hist[r.os_cur ^ 1],
-                                 r.os_status, r.os_ctr, r.os_epoch, r.os_ctr + lsb::kOnesweepSubs,
-                                 r.os_grid, r.stream, extra));
-    if (c->timing) c->scatter_elems += m;
-  }
-  std::swap(r.A, r.B);
+  LSB_TRY(onesweep_launch(c, r, shift, next, hist[r.os_cur], hist[r.os_cur ^ 1], extra));
   if (next >= 0) {
     r.os_cur ^= 1;
     r.os_valid = next;
@@ -1028,6 +1085,8 @@ int gather_span(lsb_ctx* c, uint64_t* kor, uint64_t* knor);
 
 int sort_exchange_onesweep(lsb_ctx* c) {
   const int D = 64 / c->bits, subs = c->bits / lsb::kDigitBits;
+  c->pass_cursor = 0;
+  c->cur_pass = 0;
   for (Rank& r : c->ranks) {
     HIP_TRY(hipSetDevice(r.dev));
     LSB_TRY(onesweep_ensure(r));
@@ -1048,11 +1107,6 @@ int sort_exchange_onesweep(lsb_ctx* c) {
     LSB_TRY(gather_span(c, &kor, &knor));
     varying = kor & knor;
   }
-  // gather_span syncs only the streams it reads from: each rank syncs here.
-  for (Rank& r : c->ranks) {
-    HIP_TRY(hipSetDevice(r.dev));
-    LSB_TRY(choose_halves(c, r, false));
-  }
   c->last_varying = varying;
   // Local passes in order; an exchange follows the last one of each digit.
   // A digit on which every key agrees needs neither (its stable pass and its
@@ -1072,12 +1126,31 @@ int sort_exchange_onesweep(lsb_ctx* c) {
     }
     steps.back().exch = true;
   }
+  // The stage split is decided from the first byte that is sorted on: when
+  // byte 0 is constant, that byte is counted now (its pass reads the
+  // histogram instead of counting it again).  gather_span syncs only the
+  // streams it reads from: each rank syncs in choose_halves.
+  for (Rank& r : c->ranks) {
+    HIP_TRY(hipSetDevice(r.dev));
+    if (!steps.empty() && steps[0].shift != 0 && r.here > 0) {
+      {
+        Timer t(c, &r, LSB_K_UPSWEEP);
+        HIP_TRY(lsb::launch_subhist(r.A, r.here, steps[0].shift, r.os_grid, r.os_hist, nullptr,
+                                    r.stream));
+      }
+      r.os_cur = 0;
+      r.os_valid = steps[0].shift;
+      LSB_TRY(queue_halves(c, r, r.os_hist));
+    }
+    LSB_TRY(choose_halves(c, r, false));
+  }
   for (size_t i = 0; i < steps.size(); ++i) {
     const Step& st = steps[i];
     const int after = i + 1 < steps.size() ? steps[i + 1].shift : -1;
     // 16-bit digit: its high-byte pass counts the 65536 digits (a constant
     // high byte leaves the count to digit_counts' read of A).
     const bool c16 = c->bits == 16 && st.exch && st.shift == st.digit * 16 + lsb::kDigitBits;
+    begin_pass(c, st.shift);
     for (Rank& r : c->ranks) {
       lsb::OnesweepExtra x;
       if (st.exch && c->bits == 8) x.totals = r.totals;
@@ -1274,6 +1347,8 @@ int sort_local_rank(lsb_ctx* c, Rank& r, int* passes, uint64_t* varying) {
   if (c->onesweep && r.here <= lsb::kOnesweepMaxElems) return sort_onesweep_rank(c, r, passes, varying);
   HIP_TRY(hipSetDevice(r.dev));
   HIP_TRY(hipMemsetAsync(r.span, 0, 2 * sizeof(uint64_t), r.stream));
+  c->pass_cursor = 0;
+  begin_pass(c, 0);
   LSB_TRY(local_pass(c, r, 0, c->skip_constant));
   *passes = 1;
   *varying = ~0ull;
@@ -1284,6 +1359,7 @@ int sort_local_rank(lsb_ctx* c, Rank& r, int* passes, uint64_t* varying) {
   }
   for (int d = 1; d < 64 / lsb::kDigitBits; ++d) {
     if (((*varying >> (d * lsb::kDigitBits)) & (lsb::kBuckets - 1)) == 0) continue;
+    begin_pass(c, d * lsb::kDigitBits);
     LSB_TRY(local_pass(c, r, d * lsb::kDigitBits));
     ++*passes;
   }
@@ -1846,6 +1922,8 @@ int lsb_copy_out(lsb_ctx_t* c, int rank, int64_t off, int64_t cnt, lsb_elem_t* h
 int lsb_pass(lsb_ctx_t* c, int digit) {
   LSB_TRY(check_ctx(c));
   if (digit < 0 || digit >= 64 / c->bits) return fail(LSB_ERR_INVALID, "lsb_pass", "digit");
+  // Filed under the digit's own local passes (a 64-bit digit: the whole sort).
+  c->pass_cursor = c->bits == 64 ? 0 : digit * (c->bits / lsb::kDigitBits);
   return do_pass(c, digit);
 }
 
@@ -1857,6 +1935,8 @@ int lsb_sort(lsb_ctx_t* c) {
   const int passes = 64 / c->bits;
   c->last_local_passes = c->last_exchanges = 0;
   c->last_varying = ~0ull;
+  c->pass_cursor = 0;
+  c->cur_pass = 0;
   if (c->bits == 64 && exchanging(c)) {
     LSB_TRY(merge_sort(c));
   } else if (onesweep_applies(c)) {
@@ -1995,6 +2075,30 @@ int lsb_reset_kernel_stats(lsb_ctx_t* c) {
     c->total_ms[k] = 0.0;
   }
   c->scatter_elems = 0;
+  for (int p = 0; p < LSB_MAX_PASSES; ++p) {
+    for (int k = 0; k < LSB_K_COUNT; ++k) {
+      c->pass_launches[p][k] = 0;
+      c->pass_ms[p][k] = 0.0;
+    }
+    c->pass_elems[p] = 0;
+  }
+  return LSB_OK;
+}
+
+int lsb_get_pass_stats(lsb_ctx_t* c, int pass, int* shift, int64_t* launches, int64_t* elems,
+                       double* ms_count, double* ms_scatter, double* ms_exchange, double* ms_place) {
+  LSB_TRY(check_ctx(c));
+  if (pass < 0 || pass >= LSB_MAX_PASSES) return fail(LSB_ERR_INVALID, "lsb_get_pass_stats", "pass");
+  LSB_TRY(resolve_timing(c));
+  const bool ran = c->pass_launches[pass][LSB_K_SCATTER] > 0;
+  if (shift) *shift = ran ? c->pass_shift[pass] : -1;
+  if (launches) *launches = c->pass_launches[pass][LSB_K_SCATTER];
+  if (elems) *elems = c->pass_elems[pass];
+  // The count kernels: k_subhist / k_upsweep (read) and k_scan.
+  if (ms_count) *ms_count = c->pass_ms[pass][LSB_K_UPSWEEP] + c->pass_ms[pass][LSB_K_SCAN];
+  if (ms_scatter) *ms_scatter = c->pass_ms[pass][LSB_K_SCATTER];
+  if (ms_exchange) *ms_exchange = c->pass_ms[pass][LSB_K_EXCHANGE];
+  if (ms_place) *ms_place = c->pass_ms[pass][LSB_K_PLACE];
   return LSB_OK;
 }
 

@@ -89,6 +89,10 @@ struct World {
   int64_t n = 0;
   int64_t per = 0;
   int dev = 0;  // device of this process's ranks
+  // --gpus P: the failure report's gather to the root (MPI_Gather of the
+  // output, mpi/mpi_lsbsort.cpp:717-719): report_fd[r] is the root's read end
+  // of rank r's pipe; report_fd[first] a non-root rank's write end.
+  std::vector<int> report_fd;
   bool root() const { return first == 0; }
   bool is_local(int r) const { return r >= first && r < first + nlocal; }
 };
@@ -119,41 +123,93 @@ void print_array(World& w, const char* name, int64_t n_per_rank) {
   }
 }
 
-// The reference's failure report (mpi/mpi_lsbsort.cpp:722-737): every
-// index whose record differs from std::stable_sort of the input by key,
-// with the expected and the actual record.  The input is regenerated on
-// this process's device (a loopback context of the same n, P and key
-// distribution: the same on-device PCG stream the sort started from), then
-// stable-sorted here; ranks print in rank order.
+// Whole-buffer pipe I/O (the report's gather).
+bool write_all(int fd, const void* p, size_t bytes) {
+  const char* c = static_cast<const char*>(p);
+  while (bytes > 0) {
+    const ssize_t k = write(fd, c, bytes);
+    if (k <= 0) return false;
+    c += k;
+    bytes -= (size_t)k;
+  }
+  return true;
+}
+
+bool read_all(int fd, void* p, size_t bytes) {
+  char* c = static_cast<char*>(p);
+  while (bytes > 0) {
+    const ssize_t k = read(fd, c, bytes);
+    if (k <= 0) return false;
+    c += k;
+    bytes -= (size_t)k;
+  }
+  return true;
+}
+
+constexpr int64_t kReportChunk = 1 << 20;  // records per pipe transfer
+
+// The reference's failure report (mpi/mpi_lsbsort.cpp:715-737): the output
+// is gathered to the root, which compares every index with std::stable_sort
+// of the input by key and prints each mismatch with the expected and the
+// actual record.  Only the root regenerates the input (a loopback context of
+// the same n, P and key distribution on its device: the on-device PCG stream
+// the sort started from) and sorts it on the host: host memory O(n) once, as
+// the reference's rank 0.  The other rank processes stream their records to
+// it through pipes, in rank order; there is no collective in the report.
 void report_mismatches(World& w, const Options& o) {
-  lsb_ctx_t* gen = nullptr;
-  std::vector<int> devs(w.P, w.dev);
-  CHECK(lsb_create(&gen, o.n, w.P, devs.data(), 8));
-  CHECK(lsb_generate_ex(gen, o.dist, o.zipf_s));
+  std::vector<lsb_elem_t> got;
+  if (!w.root()) {  // --gpus: send my part to the root
+    const int64_t here = lsb_here(o.n, w.P, w.first);
+    const int fd = w.report_fd[w.first];
+    if (!write_all(fd, &here, sizeof here)) die("report: write", LSB_ERR_STATE);
+    for (int64_t off = 0; off < here; off += kReportChunk) {
+      const int64_t k = std::min(kReportChunk, here - off);
+      got.resize((size_t)k);
+      CHECK(lsb_copy_out(w.ctx, w.first, off, k, got.data()));
+      if (!write_all(fd, got.data(), (size_t)k * sizeof(lsb_elem_t))) die("report: write", LSB_ERR_STATE);
+    }
+    close(fd);
+    return;
+  }
   std::vector<lsb_elem_t> expect((size_t)o.n);
-  for (int r = 0; r < w.P; ++r)
-    CHECK(lsb_copy_out(gen, r, 0, lsb_here(o.n, w.P, r), expect.data() + (size_t)r * w.per));
-  lsb_destroy(gen);
+  {
+    lsb_ctx_t* gen = nullptr;
+    std::vector<int> devs(w.P, w.dev);
+    CHECK(lsb_create(&gen, o.n, w.P, devs.data(), 8));
+    CHECK(lsb_generate_ex(gen, o.dist, o.zipf_s));
+    for (int r = 0; r < w.P; ++r)
+      CHECK(lsb_copy_out(gen, r, 0, lsb_here(o.n, w.P, r), expect.data() + (size_t)r * w.per));
+    lsb_destroy(gen);
+  }
   std::stable_sort(expect.begin(), expect.end(),
                    [](const lsb_elem_t& a, const lsb_elem_t& b) { return a.key < b.key; });
-  std::vector<lsb_elem_t> got;
   for (int r = 0; r < w.P; ++r) {
-    CHECK(lsb_barrier(w.ctx));
-    if (!w.is_local(r)) continue;
     const int64_t here = lsb_here(o.n, w.P, r);
-    got.resize((size_t)here);
-    CHECK(lsb_copy_out(w.ctx, r, 0, here, got.data()));
-    for (int64_t i = 0; i < here; ++i) {
-      const lsb_elem_t& e = expect[(size_t)(r * w.per + i)];
-      const lsb_elem_t& g = got[(size_t)i];
-      if (e.key == g.key && e.val == g.val) continue;
-      printf("Sorted element %" PRId64 " did not match\n", r * w.per + i);
-      printf("Expected: (%016" PRIx64 ",%" PRIu64 ")\n", e.key, e.val);
-      printf("Got:      (%016" PRIx64 ",%" PRIu64 ")\n", g.key, g.val);
+    int64_t sent = here;
+    if (!w.is_local(r) && !read_all(w.report_fd[r], &sent, sizeof sent)) {
+      printf("Rank %d sent no records\n", r);
+      continue;
     }
-    flush_output();
+    if (sent != here) die("report: record count", LSB_ERR_STATE);
+    for (int64_t off = 0; off < here; off += kReportChunk) {
+      const int64_t k = std::min(kReportChunk, here - off);
+      got.resize((size_t)k);
+      if (w.is_local(r)) CHECK(lsb_copy_out(w.ctx, r, off, k, got.data()));
+      else if (!read_all(w.report_fd[r], got.data(), (size_t)k * sizeof(lsb_elem_t)))
+        die("report: read", LSB_ERR_STATE);
+      for (int64_t i = 0; i < k; ++i) {
+        const int64_t gi = r * w.per + off + i;
+        const lsb_elem_t& e = expect[(size_t)gi];
+        const lsb_elem_t& g = got[(size_t)i];
+        if (e.key == g.key && e.val == g.val) continue;
+        printf("Sorted element %" PRId64 " did not match\n", gi);
+        printf("Expected: (%016" PRIx64 ",%" PRIu64 ")\n", e.key, e.val);
+        printf("Got:      (%016" PRIx64 ",%" PRIu64 ")\n", g.key, g.val);
+      }
+    }
+    if (!w.is_local(r)) close(w.report_fd[r]);
   }
-  CHECK(lsb_barrier(w.ctx));
+  flush_output();
 }
 
 int run(World& w, const Options& o) {
@@ -248,7 +304,8 @@ int run(World& w, const Options& o) {
   return status;
 }
 
-int run_rank_process(const Options& o, int rank, int read_fd, const std::vector<int>& write_fds) {
+int run_rank_process(const Options& o, int rank, int read_fd, const std::vector<int>& write_fds,
+                     const std::vector<int>& report_fd) {
   int dev = rank;
   if (o.share_gpus > 0) {
     // Before anything touches RCCL: one host per rank, linked over loopback.
@@ -279,6 +336,7 @@ int run_rank_process(const Options& o, int rank, int read_fd, const std::vector<
   w.first = rank;
   w.nlocal = 1;
   w.dev = dev;
+  w.report_fd = report_fd;
   CHECK(lsb_create_rank(&w.ctx, o.n, o.gpus, rank, dev, o.radix_bits, id));
   const int status = run(w, o);
   lsb_destroy(w.ctx);
@@ -345,6 +403,17 @@ int main(int argc, char* argv[]) {
       rd[r] = fds[0];
       wr[r] = fds[1];
     }
+    // Report pipes (verify failure only): rank q > 0 -> the root.
+    std::vector<int> rep_rd(o.gpus, -1), rep_wr(o.gpus, -1);
+    for (int r = 1; r < o.gpus; ++r) {
+      int fds[2];
+      if (pipe(fds) != 0) {
+        perror("pipe");
+        return 2;
+      }
+      rep_rd[r] = fds[0];
+      rep_wr[r] = fds[1];
+    }
     std::vector<pid_t> kids;
     for (int r = 0; r < o.gpus; ++r) {
       pid_t pid = fork();
@@ -356,11 +425,24 @@ int main(int argc, char* argv[]) {
         std::vector<int> mine;
         if (r == 0)
           for (int q = 1; q < o.gpus; ++q) mine.push_back(wr[q]);
-        const int st = run_rank_process(o, r, rd[r], mine);
+        // Keep only my ends of the report pipes, so the root sees EOF from a
+        // rank that died instead of waiting on it.
+        std::vector<int> rep(o.gpus, -1);
+        for (int q = 1; q < o.gpus; ++q) {
+          if (r == 0) rep[q] = rep_rd[q];
+          else close(rep_rd[q]);
+          if (q == r) rep[q] = rep_wr[q];
+          else close(rep_wr[q]);
+        }
+        const int st = run_rank_process(o, r, rd[r], mine, rep);
         fflush(stdout);
         _exit(st);
       }
       kids.push_back(pid);
+    }
+    for (int q = 1; q < o.gpus; ++q) {
+      close(rep_rd[q]);
+      close(rep_wr[q]);
     }
     int worst = 0;
     for (pid_t pid : kids) {

@@ -50,6 +50,7 @@ OPT_EXCHANGE_PEER = 5
 OPT_ONESWEEP = 6
 OPT_EXCHANGE_SELF = 7
 OPT_ONESWEEP_SPLIT = 8
+MAX_PASSES = 16
 
 
 class LsbError(RuntimeError):
@@ -155,6 +156,9 @@ def _lib() -> ctypes.CDLL:
             "lsb_get_kernel_stats": (i32, [vp, i32, P64, ctypes.POINTER(ctypes.c_double)]),
             "lsb_reset_kernel_stats": (i32, [vp]),
             "lsb_get_scatter_elems": (i32, [vp, P64]),
+            "lsb_get_pass_stats": (i32, [vp, i32, ctypes.POINTER(ctypes.c_int), P64, P64,
+                                         ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                         ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
             "lsb_get_exchange_bytes": (i32, [vp, P64, P64, P64]),
             "lsb_build_info": (cp, []),
             "lsb_plan_exchange": (i32, [i64, i32, i32, i32, vp, vp, vp, vp, vp, vp]),
@@ -434,6 +438,23 @@ class World:
             _check(_lib().lsb_get_kernel_stats(self._h, kid, ctypes.byref(n), ctypes.byref(ms)),
                    "lsb_get_kernel_stats")
             out[name] = (int(n.value), float(ms.value))
+        return out
+
+    def pass_stats(self) -> list:
+        """Per local pass that ran since the last reset (lsb_get_pass_stats):
+        dicts with pass, shift, launches, elems and the device ms of its count,
+        scatter, exchange and placement work, summed over launches."""
+        out = []
+        for p in range(MAX_PASSES):
+            sh, la, el = ctypes.c_int(), ctypes.c_int64(), ctypes.c_int64()
+            ms = [ctypes.c_double() for _ in range(4)]
+            _check(_lib().lsb_get_pass_stats(self._h, p, ctypes.byref(sh), ctypes.byref(la), ctypes.byref(el),
+                                             *[ctypes.byref(x) for x in ms]), "lsb_get_pass_stats")
+            if sh.value < 0:
+                continue
+            out.append({"pass": p, "shift": int(sh.value), "launches": int(la.value), "elems": int(el.value),
+                        "ms_count": ms[0].value, "ms_scatter": ms[1].value, "ms_exchange": ms[2].value,
+                        "ms_place": ms[3].value})
         return out
 
     def reset_kernel_stats(self) -> None:

@@ -209,6 +209,20 @@ int  lsb_get_kernel_stats(lsb_ctx_t* ctx, int kernel_id, int64_t* launches, doub
 int  lsb_reset_kernel_stats(lsb_ctx_t* ctx);
 /* Elements one launch of the scatter kernel processed, summed like the stats. */
 int  lsb_get_scatter_elems(lsb_ctx_t* ctx, int64_t* elems);
+/* The same stats per local pass (the reference times only the
+ * whole sort, mpi/mpi_lsbsort.cpp:688-699).  Pass p is the p-th 8-bit local
+ * pass a sort ran (0-based; constant digits are skipped, so p counts passes
+ * that ran, not digits; lsb_pass files a digit's passes under its own index).
+ * A sort's first count read is filed under its first pass, and an exchange
+ * (all-gather, plan, all-to-all, placement or merge) under the local pass
+ * before it.  Summed over the launches since the last reset, every local
+ * rank included: *shift = the pass's key shift (-1: no launch), *launches /
+ * *elems = scatter launches and the records they processed, and the device
+ * milliseconds of its count kernels (k_subhist / k_upsweep + k_scan), its
+ * scatter (k_onesweep or k_scatter), its exchange and its placement. */
+#define LSB_MAX_PASSES 16
+int  lsb_get_pass_stats(lsb_ctx_t* ctx, int pass, int* shift, int64_t* launches, int64_t* elems,
+                        double* ms_count, double* ms_scatter, double* ms_exchange, double* ms_place);
 /* Element payload this context handed to its all-to-all collective
  * (ncclAllToAllv, grouped ncclSend/ncclRecv or the caller's alltoallv) since
  * the context was created: calls, bytes sent (self segment included when

@@ -28,3 +28,69 @@ def test_cpu_baseline_times_the_reference():
     assert r["kind"] == "reference" and r["n"] == 1 << 20 and r["n_basis"] == "requested"
     assert r["ranks"] >= 5 and r["cores_used"] == r["ranks"]  # >= 5 ranks
     assert len(r["runs"]) == 1 and r["value"] == r["median"] > 0
+
+
+# ---- the N > 1 launch (no GPU: --dry-rank runs the plumbing only) ----------
+# `python bench.py --gpus N` without a launcher starts the N rank processes
+# itself, as `mpirun -n N` starts the reference's ranks (mpi/README.md:24-28);
+# under torch.distributed.run the launcher's processes are the ranks.  Either
+# way the whole-key extra runs in fresh processes after the headline.
+def _bench(args, env=None, timeout=240):
+    import subprocess
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True,
+                          text=True, timeout=timeout, cwd=ROOT, env=env)
+
+
+def _line(stdout):
+    import json
+    lines = [l for l in stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, stdout
+    return json.loads(lines[0])
+
+
+def test_self_launch_relays_rank0_line():
+    r = _bench(["--gpus", "3", "--dry-rank", "--no-cpu-baseline"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = _line(r.stdout)
+    assert out["n_gpus"] == 3 and out["max_rank"] == 2.0  # all three ranks joined one group
+    assert out["launcher"].startswith("bench.py started 3 rank processes")
+    # the whole-key extra ran in its own rank processes, with the 64-bit digit
+    assert out["whole_key_melem_s"] == 3 * 64 and out["whole_key_verified"] is True
+    assert out["cpu_baseline"] is None
+
+
+def test_self_launch_fails_with_the_failing_rank():
+    r = _bench(["--gpus", "2", "--dry-rank", "--dry-fail", "1", "--no-cpu-baseline"])
+    assert r.returncode == 1
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert "rank exit codes" in r.stderr and "rank 1" in r.stderr
+
+
+def test_whole_key_failure_keeps_the_headline():
+    r = _bench(["--gpus", "2", "--dry-rank", "--dry-fail-whole-key", "0", "--no-cpu-baseline"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = _line(r.stdout)
+    assert out["value"] == 2 * 16 and "whole_key_melem_s" not in out
+    assert "whole_key_error" in out and "rank exit codes" in out["whole_key_error"]
+
+
+@pytest.mark.parametrize("fail_extra", [False, True])
+def test_torchrun_ranks_run_the_extra_in_child_processes(fail_extra):
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--dry-rank", "--no-cpu-baseline"]
+    if fail_extra:
+        cmd += ["--dry-fail-whole-key", "1"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = _line(r.stdout)
+    assert out["n_gpus"] == 2 and out["value"] == 32.0
+    if fail_extra:  # every rank agreed the extra failed; the headline stands
+        assert "whole_key_error" in out and "whole_key_melem_s" not in out
+    else:
+        assert out["whole_key_melem_s"] == 128.0

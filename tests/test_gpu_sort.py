@@ -155,14 +155,15 @@ def _masked_keys(n, mask, rng):
 
 # (key mask, radix bits, P) -> 8-bit local passes and exchanges lsb_sort must
 # run, with reduce-then-scan passes (digit 0 always runs: the key span comes
-# out of its count kernel) and with single-read passes (P = 1 runs digit 0
-# too; the per-digit exchange forms read the span with k_subhist before any
-# pass, so a constant digit 0 is skipped like any other).
+# out of its count kernel) and with single-read passes (k_subhist reads the
+# span before any pass, so a constant digit 0 is skipped like any other, at
+# P = 1 too).
 @pytest.mark.parametrize("mask,bits,P,passes,exchanges,passes_os,exchanges_os", [
     (0xFFFFFFFF, 8, 1, 4, 0, 4, 0),                 # keys < 2^32: bytes 4..7 constant
     (0xFFFF0000000000FF, 8, 1, 3, 0, 3, 0),         # bytes 1..5 constant
     (0xFFFFFFFFFFFFFFFF, 8, 1, 8, 0, 8, 0),         # nothing to skip
-    (0x0, 8, 1, 1, 0, 1, 0),                        # all keys 0: only the first pass
+    (0x0, 8, 1, 1, 0, 0, 0),                        # all keys 0: nothing (reduce-scan: the first pass)
+    (0xFFFFFFFFFFFFFF00, 8, 1, 8, 0, 7, 0),         # byte 0 constant (keys multiples of 256)
     (0x0000000000FFFFFF, 8, 3, 3, 3, 3, 3),         # 3 digits, each with its exchange
     (0x0000000000FFFFFF, 16, 3, 3, 2, 3, 2),        # 16-bit: digits 0,1; byte 3 skipped
     (0xFF00000000000000, 16, 4, 3, 2, 1, 1),        # 16-bit: digit 3's high byte (+ digit 0 forced)
@@ -394,6 +395,52 @@ def test_kernel_stats(lsb_built, onesweep):
         assert w.scatter_elems() == 8 << 20
 
 
+@pytest.mark.parametrize("onesweep", [1, 0])
+def test_pass_stats(lsb_built, onesweep):
+    """lsb_get_pass_stats: one row per local pass, in order,
+    whose scatter times add up to the kernel totals."""
+    n = 1 << 20
+    with lsb_built.World(n, ranks=1) as w:
+        w.set_option(lsb_built.OPT_ONESWEEP, onesweep)
+        w.generate()
+        w.set_timing(True)
+        for _ in range(2):
+            w.my_sort()
+        rows = w.pass_stats()
+        st = w.kernel_stats()
+        assert [r["pass"] for r in rows] == list(range(8))
+        assert [r["shift"] for r in rows] == [8 * p for p in range(8)]
+        assert all(r["launches"] == 2 and r["elems"] == 2 * n and r["ms_scatter"] > 0 for r in rows)
+        assert sum(r["ms_scatter"] for r in rows) == pytest.approx(st["scatter"][1], rel=1e-9)
+        assert sum(r["ms_count"] for r in rows) == pytest.approx(st["upsweep"][1] + st["scan"][1], rel=1e-9)
+        # single-read passes: the one count read per sort is filed under pass 0
+        assert (rows[0]["ms_count"] > 0) and all((r["ms_count"] > 0) == (not onesweep) for r in rows[1:])
+        assert all(r["ms_exchange"] == 0 and r["ms_place"] == 0 for r in rows)
+        w.reset_kernel_stats()
+        assert w.pass_stats() == []
+
+
+def test_pass_stats_exchange_and_skipped_digits(lsb_built, oracle_mod):
+    """Exchanges are filed under the local pass before them; constant bytes
+    are not passes (keys < 2^24: bytes 0-2 vary)."""
+    rng = np.random.default_rng(3)
+    a = _masked_keys(200_003, 0xFFFFFF, rng)
+    with lsb_built.World(a.size, ranks=2, radix_bits=16) as w:
+        w.scatter_global(a)
+        w.set_timing(True)
+        w.my_sort()
+        assert np.array_equal(w.gather_global(), oracle_mod.stable_sort(a))
+        rows = w.pass_stats()
+        assert [r["shift"] for r in rows] == [0, 8, 16]
+        # 16-bit exchange digits: after byte 1 (digit 0) and byte 2 (digit 1)
+        assert [r["ms_exchange"] > 0 for r in rows] == [False, True, True]
+        assert [r["ms_place"] > 0 for r in rows] == [False, True, True]
+        assert all(r["elems"] == a.size for r in rows)  # both ranks' records
+    with pytest.raises(lsb_built.LsbError):
+        lsb_built._check(lsb_built._lib().lsb_get_pass_stats(None, 0, None, None, None, None, None, None,
+                                                             None), "null context")
+
+
 def _rebalanced_hist(rng, P, nb, n, here, skew):
     """Random P x nb count matrix whose row r sums to here(n, P, r)."""
     if skew:
@@ -573,12 +620,15 @@ def test_zipf_verify_uses_zipf_keys(lsb_built):
         assert w.verify() == (True, -1)
 
 
-@pytest.mark.parametrize("mode", [["--ranks", "3"], ["--gpus", "1"]])
+@pytest.mark.parametrize("mode", [["--ranks", "3"], ["--gpus", "1"], ["--gpus", "2", "--share-gpus", "1"],
+                                  ["--gpus", "3", "--share-gpus", "1"]])
 def test_harness_reports_every_mismatch(lsb_built, oracle_mod, mode):
     """A failed verify prints every bad index with Expected/Got, as the
     reference does (mpi/mpi_lsbsort.cpp:729-737), and exits like its failed
-    assert (134)."""
-    n, bad = 5000, 1234
+    assert (134).  With --gpus P the bad record sits on the last rank, whose
+    process streams its records to the root (the reference's gather to rank 0,
+    :715-719); only the root regenerates and sorts the input."""
+    n, bad = 5000, 3766
     exe = lsb_built.HARNESS_PATH
     r = subprocess.run([exe, "--n", str(n), "--verify", "--test-corrupt", str(bad)] + mode,
                        capture_output=True, text=True, timeout=300)

@@ -1,0 +1,60 @@
+#!/bin/bash
+# One GPU check of the tree (run from the repo root on the GPU box):
+#   TAG=r03_v1 STEPS="tests smoke bench n2 n4zipf torchrun profile sq" bash tools/gpu_round.sh
+# Steps (each under its own time limit; the first failure ends the call):
+#   tests     the whole -m gpu suite
+#   smoke     __graft_entry__.smoke()
+#   bench     bench.py at N = 1 (live PMC traffic + CPU baseline)
+#   n2        bench.py --gpus 2 with no launcher over RCCL's socket transport
+#             (two rank processes on the one GPU: the N > 1 code path, not a speed)
+#   n4zipf    the same at N = 4 with Zipf keys
+#   torchrun  bench.py --gpus 2 under torch.distributed.run (the driver's form)
+#   profile   tools/profile.sh: rocprofv3 stats + FETCH_SIZE / WRITE_SIZE passes
+#   sq        tools/sq_counters.sh: SQ counters of the sort at 2^28
+# Output under gpurun_out/$TAG/.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+TAG=${TAG:-check}
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+cd $R
+STEPS=${STEPS:-"tests smoke bench"}
+fail() { echo "FAILED: $1"; tail -40 "$2"; exit 1; }
+for s in $STEPS; do
+  echo "== $s $(date +%T)"
+  case $s in
+    tests)
+      timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+        > $O/gputests.log 2>&1 || fail tests $O/gputests.log
+      tail -2 $O/gputests.log ;;
+    smoke)
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 \
+        || fail smoke $O/smoke.log
+      tail -1 $O/smoke.log ;;
+    bench)
+      timeout -k 10 500 python -u bench.py > $O/bench.log 2>&1 || fail bench $O/bench.log
+      tail -1 $O/bench.log | cut -c1-400 ;;
+    n2)
+      timeout -k 10 400 python -u bench.py --gpus 2 --transport rccl-sockets --n-per-gpu 67108864 \
+        --steps 2 --warmup 1 --no-cpu-baseline > $O/bench_n2.log 2>&1 || fail n2 $O/bench_n2.log
+      tail -1 $O/bench_n2.log | cut -c1-400 ;;
+    n4zipf)
+      timeout -k 10 400 python -u bench.py --gpus 4 --transport rccl-sockets --dist zipf \
+        --n-per-gpu 16777216 --steps 2 --warmup 1 --no-cpu-baseline > $O/bench_n4_zipf.log 2>&1 \
+        || fail n4zipf $O/bench_n4_zipf.log
+      tail -1 $O/bench_n4_zipf.log | cut -c1-400 ;;
+    torchrun)
+      timeout -k 10 400 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+        --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --transport rccl-sockets \
+        --n-per-gpu 67108864 --steps 2 --warmup 1 --no-cpu-baseline > $O/bench_torchrun_n2.log 2>&1 \
+        || fail torchrun $O/bench_torchrun_n2.log
+      grep '^{' $O/bench_torchrun_n2.log | tail -1 | cut -c1-400 ;;
+    profile)
+      bash tools/profile.sh > $O/profile.log 2>&1 || fail profile $O/profile.log
+      cp $(find gpurun_out/prof/stats -name "*kernel_stats.csv" -print -quit) $O/kernel_stats.csv || true ;;
+    sq)
+      SQ_TAG=_$TAG bash tools/sq_counters.sh > $O/sq.log 2>&1 || fail sq $O/sq.log ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo "done $(date +%T)"

@@ -14,8 +14,12 @@ Output: the reference's golden digest for `mpirun -n P mpi_lsbsort --n n`
 where one exists (tests/golden/digests.json), plus the on-device verify and
 checkSorted of every rank.
 
-    python tools/rccl_two_ranks.py [radix_bits] [n] [world] [exchange] [slices]
+    python tools/rccl_two_ranks.py [radix_bits] [n] [world] [exchange] [slices] [dist] [dump_dir]
       exchange: alltoallv (default) | p2p
+      dist:     uniform (default) | zipf (s = 1.1)
+      dump_dir: each rank writes its input and sorted output there as
+                in_<r>.npy / out_<r>.npy (the tests compare them with the
+                oracle's stable sort: Zipf input has no reference digest)
 """
 import hashlib
 import json
@@ -27,7 +31,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "distributed-lsb_amd"))
 
 
-def worker(rank, world, n, bits, exchange, slices, q_uid, q_out):
+def worker(rank, world, n, bits, exchange, slices, dist, dump, q_uid, q_out):
     # One "host" per rank, before anything touches RCCL.
     os.environ["NCCL_HOSTID"] = f"lsb-rank-{rank}"
     os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
@@ -46,7 +50,10 @@ def worker(rank, world, n, bits, exchange, slices, q_uid, q_out):
             w.set_option(lsbsort.OPT_EXCHANGE_P2P, 1)
         if slices:
             w.set_option(lsbsort.OPT_EXCHANGE_SLICES, slices)
-        w.generate()
+        w.generate(dist)
+        if dump:
+            import numpy as np
+            np.save(os.path.join(dump, f"in_{rank}.npy"), w.copy_out(rank))
         w.barrier()
         w.my_sort()
         w.barrier()
@@ -54,6 +61,9 @@ def worker(rank, world, n, bits, exchange, slices, q_uid, q_out):
         sorted_ = w.check_sorted()
         _, xbytes, xmax = w.exchange_bytes()
         out = w.copy_out(rank)
+        if dump:
+            import numpy as np
+            np.save(os.path.join(dump, f"out_{rank}.npy"), out)
         w.close()
         q_out.put((rank, "ok", ok, bad, sorted_, out.tobytes(), xbytes, xmax))
     except Exception as e:  # report, never hang the parent
@@ -66,9 +76,11 @@ def main():
     world = int(sys.argv[3]) if len(sys.argv) > 3 else 2
     exchange = sys.argv[4] if len(sys.argv) > 4 else "alltoallv"
     slices = int(sys.argv[5]) if len(sys.argv) > 5 else 0
+    dist = sys.argv[6] if len(sys.argv) > 6 else "uniform"
+    dump = sys.argv[7] if len(sys.argv) > 7 else ""
     ctx = mp.get_context("spawn")
     q_uid, q_out = ctx.Queue(), ctx.Queue()
-    procs = [ctx.Process(target=worker, args=(r, world, n, bits, exchange, slices, q_uid, q_out))
+    procs = [ctx.Process(target=worker, args=(r, world, n, bits, exchange, slices, dist, dump, q_uid, q_out))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -84,11 +96,13 @@ def main():
         sys.exit(1)
     digest = hashlib.sha256(b"".join(res[r][5] for r in range(world))).hexdigest()
     golden = json.load(open(os.path.join(ROOT, "tests", "golden", "digests.json")))
-    want = next((g["output"] for g in golden["rows"] if g["n"] == n and g["P"] == world), None)
+    want = None if dist != "uniform" else next(
+        (g["output"] for g in golden["rows"] if g["n"] == n and g["P"] == world), None)
     verify = [res[r][2] for r in range(world)]
     sorted_ = [res[r][4] for r in range(world)]
     good = all(verify) and all(sorted_) and (want is None or digest == want)
     print(json.dumps({"status": "ok" if good else "mismatch", "radix_bits": bits, "n": n, "world": world,
+                      "dist": dist,
                       "exchange": exchange, "slices": slices or "default", "verify": verify,
                       "check_sorted": sorted_, "rccl_bytes": [res[r][6] for r in range(world)],
                       "rccl_max_call_bytes": [res[r][7] for r in range(world)], "digest": digest,
