@@ -93,8 +93,12 @@ def parse():
                     help="N > 1 element exchange: RCCL AllToAllv in slices (default), grouped "
                          "ncclSend/ncclRecv, or direct peer stores into the owners' buffers")
     ap.add_argument("--zipf-s", type=float, default=1.1)
-    ap.add_argument("--passes", choices=("onesweep", "reduce-scan"), default="onesweep",
-                    help="local pass form: single-read (look-back) or count + scan + scatter")
+    ap.add_argument("--passes", choices=("onesweep", "reduce-scan", "hybrid"), default="onesweep",
+                    help="local pass form: single-read (look-back), count + scan + scatter, or the "
+                         "hybrid (single-read passes on the top bytes, then one segmented local sort; "
+                         "LSB_OPT_HYBRID, P = 1 and the whole-key form's local sorts)")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the extra forms timed after the headline (hybrid at N = 1, whole key at N > 1)")
     return ap.parse_args()
 
 
@@ -394,7 +398,8 @@ def make_world(a, d, N, n_total, radix):
         w.set_option(lsbsort.OPT_EXCHANGE_P2P, 1)
     elif a.exchange == "peer" and radix != 64:
         w.set_option(lsbsort.OPT_EXCHANGE_PEER, 1)
-    w.set_option(lsbsort.OPT_ONESWEEP, 1 if a.passes == "onesweep" else 0)
+    w.set_option(lsbsort.OPT_ONESWEEP, 0 if a.passes == "reduce-scan" else 1)
+    w.set_option(lsbsort.OPT_HYBRID, 1 if a.passes == "hybrid" else 0)
     return w, device
 
 
@@ -506,25 +511,37 @@ def last_json(text):
     return json.loads(lines[-1]) if lines else None
 
 
+def extra_argv(a, flags, steps=3):
+    """The command line of an extra form: this run's flags plus `flags`,
+    fewer steps, no extras or CPU baseline of its own."""
+    return sys.argv[1:] + flags + ["--steps", str(min(a.steps, steps)), "--warmup", "1",
+                                   "--no-cpu-baseline", "--no-extras", "--no-traffic"]
+
+
 def whole_key_argv(a):
-    """The command line of the whole-key extra: this run's flags with the
-    64-bit exchange digit, fewer steps, no extras of its own."""
-    argv = sys.argv[1:] + ["--radix-bits", "64", "--steps", str(min(a.steps, 3)), "--warmup", "1",
-                           "--no-cpu-baseline", "--no-whole-key", "--no-traffic"]
-    if a.exchange == "peer":  # a per-digit form; the whole key goes by AllToAllv
-        argv += ["--exchange", "alltoallv"]
-    return argv
+    """The whole-key extra: the 64-bit exchange digit (a per-digit --exchange
+    peer becomes AllToAllv)."""
+    return extra_argv(a, ["--radix-bits", "64"] + (["--exchange", "alltoallv"] if a.exchange == "peer" else []))
+
+
+def merge_extra(out, name, ok, text, report):
+    """An extra form's keys into the headline line: <name>_melem_s,
+    _ms_per_step, _verified (and its per-pass rows and dominant-kernel
+    roofline when it has them), or <name>_error."""
+    r = last_json(text) if ok else None
+    if r is None:
+        out[f"{name}_error"] = report or "no result line"
+        return
+    out[f"{name}_melem_s"] = r["value"]
+    out[f"{name}_ms_per_step"] = r["ms_per_step"]
+    out[f"{name}_verified"] = r["verified"]
+    for k in ("per_pass", "kernel_ms_per_step", "roofline"):
+        if r.get(k) is not None:
+            out[f"{name}_{k}"] = r[k]
 
 
 def merge_whole_key(out, ok, text, report):
-    """The extra's keys into the headline line."""
-    r = last_json(text) if ok else None
-    if r is None:
-        out["whole_key_error"] = report or "no result line"
-        return
-    out["whole_key_melem_s"] = r["value"]
-    out["whole_key_ms_per_step"] = r["ms_per_step"]
-    out["whole_key_verified"] = r["verified"]
+    merge_extra(out, "whole_key", ok, text, report)
 
 
 def rank_whole_key(a, d, out):
@@ -554,7 +571,7 @@ def dry_run(a):
     out = {"metric": METRIC, "value": float(d.world * radix), "ms_per_step": 1.0, "verified": True,
            "n_gpus": d.world, "max_rank": top, "radix_bits": radix,
            "config": {"n_total": a.n_per_gpu * d.world}}
-    if d.world > 1 and radix != 64 and not a.no_whole_key:
+    if d.world > 1 and radix != 64 and not (a.no_whole_key or a.no_extras):
         rank_whole_key(a, d, out)
     d.barrier()
     d.close()
@@ -568,7 +585,7 @@ def launch(a):
     torch.distributed.run would), relay rank 0's line.  Nothing in this
     process initialises HIP."""
     N = a.gpus
-    argv = sys.argv[1:] + ["--no-cpu-baseline", "--no-whole-key"]
+    argv = sys.argv[1:] + ["--no-cpu-baseline", "--no-extras"]
     port = free_port()
     ok, text, report = spawn_ranks(argv, [rank_env(r, N, r, port) for r in range(N)], a.rank_timeout,
                                    "headline")
@@ -578,7 +595,7 @@ def launch(a):
         sys.exit(1)
     out["launcher"] = f"bench.py started {N} rank processes (one per GPU)"
     radix = a.radix_bits or 16
-    if radix != 64 and not a.no_whole_key:
+    if radix != 64 and not (a.no_whole_key or a.no_extras):
         port = free_port()
         merge_whole_key(out, *spawn_ranks(whole_key_argv(a), [rank_env(r, N, r, port) for r in range(N)],
                                           a.rank_timeout, "whole-key extra"))
@@ -592,7 +609,8 @@ def probe(a):
     """One sort of the workload, nothing printed: the program rocprofv3's
     --pmc passes run (measure_traffic)."""
     w = lsbsort.World(a.n_per_gpu, ranks=1, radix_bits=a.radix_bits or 8)
-    w.set_option(lsbsort.OPT_ONESWEEP, 1 if a.passes == "onesweep" else 0)
+    w.set_option(lsbsort.OPT_ONESWEEP, 0 if a.passes == "reduce-scan" else 1)
+    w.set_option(lsbsort.OPT_HYBRID, 1 if a.passes == "hybrid" else 0)
     w.generate(a.dist, a.zipf_s)
     w.my_sort()
     w.sync()
@@ -609,7 +627,7 @@ def per_pass_rows(passes, steps, kernel, N):
             continue
         avg = p["ms_scatter"] / p["launches"]
         gbs = SCATTER_BYTES_PER_ELEM * (p["elems"] / p["launches"]) / (avg / 1e3) / 1e9 if avg > 0 else 0.0
-        row = {"pass": p["pass"], "shift": p["shift"], "kernel": kernel,
+        row = {"pass": p["pass"], "shift": p["shift"], "kernel": "k_segsort" if p["shift"] == 64 else kernel,
                "ms": round(p["ms_scatter"] / steps, 4), "gbs": round(gbs, 1),
                "frac": round(gbs / HBM_PEAK_GBS, 4)}
         if p["ms_count"]:
@@ -640,7 +658,7 @@ def main():
     # Dominant kernel: the local pass.  Single-read passes (k_onesweep) in
     # every form: P = 1, the per-digit exchange (the exchange's placement
     # counts the next pass's histogram) and each rank of the whole-key form.
-    kernel = "k_onesweep" if a.passes == "onesweep" else "k_scatter"
+    kernel = "k_scatter" if a.passes == "reduce-scan" else "k_onesweep"
 
     total, verified, step_s = timed_sorts(w, d, a, a.steps, a.warmup)
     stats = w.kernel_stats()
@@ -667,6 +685,9 @@ def main():
                     f"8-bit local passes, " +
                     (f"RCCL AllToAllv per {radix}-bit digit ({64 // radix} exchanges)" if radix != 64 else
                      "whole-key exchange digit (local sort, 1 all-to-all, merge of the P runs)"))
+    if a.passes == "hybrid":
+        workload += (" (hybrid local sort: single-read passes on the top varying bytes, then one "
+                     "segmented local sort; the same stable order)")
     if a.dist != "uniform":
         workload += f", zipf s={a.zipf_s} keys"
     if m != 1 << 30:
@@ -715,7 +736,9 @@ def main():
                  f"synthetic: zipf(s={a.zipf_s}) keys drawn from the pcg64(rank) stream (build-defined, SURVEY 8d C4)"),
         "config": {"workload": workload, "n_total": n_total, "n_per_gpu": a.n_per_gpu,
                    "local_digit_bits": 8, "local_passes": last[0], "exchanges": last[1],
-                   "pass_form": (("single-read (k_subhist once, k_onesweep per pass" +
+                   "pass_form": ("hybrid (k_subhist, k_onesweep on the top varying bytes, then one "
+                                 "k_segsort of the runs equal on them)" if a.passes == "hybrid" else
+                                 ("single-read (k_subhist once, k_onesweep per pass" +
                                   ("; k_place counts the next pass's histogram)" if N > 1 and radix != 64
                                    else ")")) if kernel == "k_onesweep"
                                  else "reduce-then-scan (k_upsweep, k_scan, k_scatter per pass)"),
@@ -744,8 +767,14 @@ def main():
         "vs_baseline_basis": "MPI mpi_lsbsort 830 M elem/s (64 nodes x 128 cores, n=2^36; BASELINE.md §1)",
         "library": lsbsort.build_info(),
     }
-    if N > 1 and radix != 64 and not a.no_whole_key:
+    if N > 1 and radix != 64 and not (a.no_whole_key or a.no_extras):
         rank_whole_key(a, d, out)
+    if N == 1 and a.passes == "onesweep" and not a.no_extras:
+        # The hybrid local sort (same output, fewer passes over HBM), in a
+        # fresh process of its own, after the headline.
+        ok, text, report = spawn_ranks(extra_argv(a, ["--passes", "hybrid"]), [dict(os.environ)],
+                                       a.rank_timeout, "hybrid extra")
+        merge_extra(out, "hybrid", ok, text, report)
     if d.rank == 0 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(n_total, a.cpu_n)
     elif d.rank == 0:

@@ -134,6 +134,16 @@ hipError_t launch_onesweep(const Elem* in, Elem* out, int64_t m, int shift, int 
                            uint32_t* tile_ctr, uint32_t epoch, uint32_t* err, int grid,
                            hipStream_t s, OnesweepExtra extra = OnesweepExtra());
 
+// Hybrid local sort (LSB_OPT_HYBRID, lsb_segsort.hip): `in` is stably sorted
+// by the bits of pmask (the top varying bytes of the key); k_segsort sorts
+// every segment (maximal run of equal key & pmask) stably by the whole key,
+// in -> out.  A segment longer than kSegMax records sets *err (output
+// invalid: the runtime sorts the kept input by the LSD passes instead).
+// grid: persistent workgroups (3 per CU).
+constexpr int kSegMax = 1024;
+hipError_t launch_segsort(const Elem* in, Elem* out, int64_t m, uint64_t pmask, uint32_t* err,
+                          int grid, hipStream_t s);
+
 // Receiver-side placement of one source's received range: src[i] (receive
 // index k0 + i) goes to out[off_row[digit] + k0 + i], off_row = the source's
 // row of the placement table (place_off[s * nbuckets ...]); out holds

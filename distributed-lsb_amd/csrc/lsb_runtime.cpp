@@ -144,6 +144,7 @@ struct lsb_ctx {
   bool onesweep = true;       // P == 1: single-read passes (k_subhist + k_onesweep)
   bool self_coll = false;     // the self segment also goes through the collective
   int os_split = 0;           // LSB_OPT_ONESWEEP_SPLIT: 0 auto, 1 never, 2 always
+  bool hybrid = false;        // LSB_OPT_HYBRID: k MSD-byte passes + k_segsort
   int64_t coll_calls = 0, coll_bytes = 0, coll_max = 0;  // element payload handed to the collective
   // What the last lsb_sort ran (lsb_get_last_sort).
   int last_local_passes = 0;
@@ -908,8 +909,8 @@ int onesweep_ensure(Rank& r) {
   LSB_TRY(dev_alloc(&r.os_status, tiles * lsb::kBuckets));
   LSB_TRY(dev_alloc(&r.os_hist, 2 * lsb::kOnesweepSubs * lsb::kBuckets));
   LSB_TRY(dev_alloc(&r.os_ctr, 2 * lsb::kOnesweepSubs));
-  LSB_TRY(host_alloc(&r.os_err_h, 1));
-  *r.os_err_h = 0;
+  LSB_TRY(host_alloc(&r.os_err_h, 2));  // [0] look-back gave up, [1] k_segsort error
+  r.os_err_h[0] = r.os_err_h[1] = 0;
   LSB_TRY(host_alloc(&r.os_hist_h, (size_t)lsb::kOnesweepSubs * lsb::kBuckets));
   HIP_TRY(hipMemsetAsync(r.os_status, 0, tiles * lsb::kBuckets * sizeof(uint32_t), r.stream));
   HIP_TRY(hipMemsetAsync(r.os_ctr, 0, 2 * lsb::kOnesweepSubs * sizeof(uint32_t), r.stream));
@@ -974,49 +975,28 @@ int choose_halves(lsb_ctx* c, Rank& r, bool synced) {
   return LSB_OK;
 }
 
-// lsb_sort when nothing is exchanged: one k_subhist read (digit 0's
-// sub-array histogram and the key span), then one k_onesweep per digit that
-// varies, each also counting the next such digit over its output.  Same
-// output as the reduce-then-scan loop (do_pass).  A constant digit 0 is
-// skipped like any other: its pass would be the identity, so the first
-// digit that varies is counted by a second k_subhist read (a read, not a
-// pass), and that digit's histogram also decides the stage split.
-// Rank r alone (its local block); *passes gets the passes it ran, *varying the
-// key bits that vary in the block.
-int sort_onesweep_rank(lsb_ctx* c, Rank& r, int* passes, uint64_t* varying) {
-  HIP_TRY(hipSetDevice(r.dev));
-  LSB_TRY(onesweep_ensure(r));
-  c->pass_cursor = 0;
-  c->cur_pass = 0;  // the count reads are filed under the first pass
-  const int64_t m = r.here;
+// k_subhist of the byte `byte` of rank r's A into os_hist[0] (the sub-array
+// histogram the first pass reads), with the key span when `span`.
+int count_byte(lsb_ctx* c, Rank& r, int byte, bool span) {
+  Timer t(c, &r, LSB_K_UPSWEEP);
+  HIP_TRY(lsb::launch_subhist(r.A, r.here, byte * lsb::kDigitBits, r.os_grid, r.os_hist,
+                              span ? r.span : nullptr, r.stream));
+  return LSB_OK;
+}
+
+// The bytes of `varying` (ascending): the digits a sort must run.
+std::vector<int> varying_bytes(uint64_t varying) {
+  std::vector<int> d;
+  for (int b = 0; b < 64 / lsb::kDigitBits; ++b)
+    if (((varying >> (b * lsb::kDigitBits)) & (lsb::kBuckets - 1)) != 0) d.push_back(b);
+  return d;
+}
+
+// One k_onesweep pass per byte of `digits` (ascending), r.A -> r.B ->
+// ..., each also counting the next byte over its output; os_hist[0] holds
+// the sub-array histogram of digits[0] over r.A.
+int onesweep_digits(lsb_ctx* c, Rank& r, const std::vector<int>& digits, int* passes) {
   uint32_t* hist[2] = {r.os_hist, r.os_hist + lsb::kOnesweepSubs * lsb::kBuckets};
-  HIP_TRY(hipMemsetAsync(r.span, 0, 2 * sizeof(uint64_t), r.stream));
-  {
-    Timer t(c, &r, LSB_K_UPSWEEP);
-    HIP_TRY(lsb::launch_subhist(r.A, m, 0, r.os_grid, hist[0], c->skip_constant ? r.span : nullptr,
-                                r.stream));
-  }
-  LSB_TRY(queue_halves(c, r, hist[0]));
-  *varying = ~0ull;
-  *passes = 0;
-  if (c->skip_constant) {
-    HIP_TRY(hipMemcpyAsync(r.span_h, r.span, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, r.stream));
-    HIP_TRY(hipStreamSynchronize(r.stream));
-    *varying = r.span_h[0] & r.span_h[1];
-  }
-  std::vector<int> digits;
-  for (int d = 0; d < 64 / lsb::kDigitBits; ++d)
-    if (((*varying >> (d * lsb::kDigitBits)) & (lsb::kBuckets - 1)) != 0) digits.push_back(d);
-  if (!digits.empty() && digits[0] != 0) {
-    Timer t(c, &r, LSB_K_UPSWEEP);
-    HIP_TRY(lsb::launch_subhist(r.A, m, digits[0] * lsb::kDigitBits, r.os_grid, hist[0], nullptr,
-                                r.stream));
-    t.stop();
-    LSB_TRY(queue_halves(c, r, hist[0]));
-    LSB_TRY(choose_halves(c, r, false));
-  } else {
-    LSB_TRY(choose_halves(c, r, c->skip_constant));
-  }
   for (size_t i = 0; i < digits.size(); ++i) {
     const int shift = digits[i] * lsb::kDigitBits;
     const int next = i + 1 < digits.size() ? digits[i + 1] * lsb::kDigitBits : -1;
@@ -1025,6 +1005,171 @@ int sort_onesweep_rank(lsb_ctx* c, Rank& r, int* passes, uint64_t* varying) {
     x.halves = r.os_halves;
     LSB_TRY(onesweep_launch(c, r, shift, next, hist[i & 1], hist[(i + 1) & 1], x));
     ++*passes;
+  }
+  return LSB_OK;
+}
+
+int sort_hybrid_rank(lsb_ctx* c, Rank& r, int* passes, uint64_t* varying);
+
+// lsb_sort when nothing is exchanged: one k_subhist read (digit 0's
+// sub-array histogram and the key span), then one k_onesweep per digit that
+// varies, each also counting the next such digit over its output.  Same
+// output as the reduce-then-scan loop (do_pass).  A constant digit 0 is
+// skipped like any other: its pass would be the identity, so the first
+// digit that varies is counted by a second k_subhist read (a read, not a
+// pass), and that digit's histogram also decides the stage split.
+// Rank r alone (its local block); *passes gets the passes it ran, *varying the
+// key bits that vary in the block.  LSB_OPT_HYBRID: sort_hybrid_rank.
+int sort_onesweep_rank(lsb_ctx* c, Rank& r, int* passes, uint64_t* varying) {
+  if (c->hybrid) return sort_hybrid_rank(c, r, passes, varying);
+  HIP_TRY(hipSetDevice(r.dev));
+  LSB_TRY(onesweep_ensure(r));
+  c->pass_cursor = 0;
+  c->cur_pass = 0;  // the count reads are filed under the first pass
+  HIP_TRY(hipMemsetAsync(r.span, 0, 2 * sizeof(uint64_t), r.stream));
+  LSB_TRY(count_byte(c, r, 0, c->skip_constant));
+  LSB_TRY(queue_halves(c, r, r.os_hist));
+  *varying = ~0ull;
+  *passes = 0;
+  if (c->skip_constant) {
+    HIP_TRY(hipMemcpyAsync(r.span_h, r.span, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, r.stream));
+    HIP_TRY(hipStreamSynchronize(r.stream));
+    *varying = r.span_h[0] & r.span_h[1];
+  }
+  const std::vector<int> digits = varying_bytes(*varying);
+  if (!digits.empty() && digits[0] != 0) {
+    LSB_TRY(count_byte(c, r, digits[0], false));
+    LSB_TRY(queue_halves(c, r, r.os_hist));
+    LSB_TRY(choose_halves(c, r, false));
+  } else {
+    LSB_TRY(choose_halves(c, r, c->skip_constant));
+  }
+  LSB_TRY(onesweep_digits(c, r, digits, passes));
+  // The look-back's give-up word, read by lsb_sync.
+  HIP_TRY(hipMemcpyAsync(r.os_err_h, r.os_ctr + lsb::kOnesweepSubs, sizeof(uint32_t),
+                         hipMemcpyDeviceToHost, r.stream));
+  return LSB_OK;
+}
+
+// ---- hybrid local sort (LSB_OPT_HYBRID) ------------------------------------
+// The same stable order as the LSD passes from fewer passes over HBM
+// (lsb_segsort.hip): k_onesweep passes on the k most significant varying
+// bytes only, then k_segsort orders every segment (run of records equal on
+// those bytes) by the whole key.  k: the fewest top varying bytes whose
+// varying bits reach ceil(log2 m), so uniform keys leave segments of about
+// one record (2^30 records: k = 4, 0.25 on average; k_segsort's walk then
+// costs ~2 LDS reads per record and the pass streams at copy speed.  k = 3,
+// 64 per segment, made k_segsort compute-bound: 69 ms against 7 for the
+// fourth byte's pass, profiles/r03_h1_probe.log).
+std::vector<int> hybrid_bytes(uint64_t varying, int64_t m) {
+  int need = 0;
+  while ((int64_t(1) << need) < m) ++need;
+  std::vector<int> top;
+  int bits = 0;
+  for (int b = 64 / lsb::kDigitBits - 1; b >= 0 && bits < need; --b) {
+    const uint64_t v = (varying >> (b * lsb::kDigitBits)) & (lsb::kBuckets - 1);
+    if (!v) continue;
+    top.insert(top.begin(), b);
+    bits += __builtin_popcountll(v);
+  }
+  return top;
+}
+
+// The hybrid for rank r.  The k passes leave the input A untouched (A -> B,
+// then B <-> R), so when k_segsort meets a segment longer than kSegMax the
+// sort starts over from A with the LSD passes; skewed keys (the first
+// pass's byte has a bucket over 1/32 of the records, as for the stage
+// split: duplicate-heavy keys make long segments) take them directly.  One
+// host sync, after k_segsort, reads its error word.
+int sort_hybrid_rank(lsb_ctx* c, Rank& r, int* passes, uint64_t* varying) {
+  HIP_TRY(hipSetDevice(r.dev));
+  LSB_TRY(onesweep_ensure(r));
+  LSB_TRY(ensure_recv(c, r));
+  c->pass_cursor = 0;
+  c->cur_pass = 0;
+  const int64_t m = r.here;
+  *passes = 0;
+  *varying = ~0ull;
+  // Count the byte the first pass most likely sorts on (full 64-bit keys)
+  // in the same read as the span.
+  const std::vector<int> guess = hybrid_bytes(~0ull, m);
+  int counted = guess.empty() ? 0 : guess[0];
+  HIP_TRY(hipMemsetAsync(r.span, 0, 2 * sizeof(uint64_t), r.stream));
+  LSB_TRY(count_byte(c, r, counted, c->skip_constant));
+  if (c->skip_constant) {
+    HIP_TRY(hipMemcpyAsync(r.span_h, r.span, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, r.stream));
+    HIP_TRY(hipStreamSynchronize(r.stream));
+    *varying = r.span_h[0] & r.span_h[1];
+  }
+  const std::vector<int> digits = varying_bytes(*varying);
+  const std::vector<int> msd = c->skip_constant ? hybrid_bytes(*varying, m) : guess;
+  bool hybrid = msd.size() < digits.size();
+  // The first byte sorted on decides the stage split and whether keys are
+  // skewed (*skewed: a bucket over 1/32 of the records).
+  auto first_hist = [&](int byte, bool* skewed) -> int {
+    if (byte != counted) {
+      LSB_TRY(count_byte(c, r, byte, false));
+      counted = byte;
+    }
+    HIP_TRY(hipMemcpyAsync(r.os_hist_h, r.os_hist, sizeof(uint32_t) * lsb::kOnesweepSubs * lsb::kBuckets,
+                           hipMemcpyDeviceToHost, r.stream));
+    HIP_TRY(hipStreamSynchronize(r.stream));
+    const int h = lsb::onesweep_halves_for(r.os_hist_h, m);
+    r.os_halves = c->os_split == 0 ? h : (c->os_split == 2 ? 2 : 1);
+    *skewed = h == 2;
+    return LSB_OK;
+  };
+  bool skewed = false;
+  if (hybrid && !msd.empty()) {
+    LSB_TRY(first_hist(msd[0], &skewed));
+    if (skewed) hybrid = false;
+  }
+  if (!hybrid) {
+    if (!digits.empty()) LSB_TRY(first_hist(digits[0], &skewed));
+    LSB_TRY(onesweep_digits(c, r, digits, passes));
+  } else {
+    // The k passes: A -> B, then B <-> R; the input X0 is kept.
+    Elem* const X0 = r.A;
+    Elem* const X1 = r.B;
+    Elem* const X2 = r.R;
+    uint32_t* hist[2] = {r.os_hist, r.os_hist + lsb::kOnesweepSubs * lsb::kBuckets};
+    for (size_t i = 0; i < msd.size(); ++i) {
+      const int shift = msd[i] * lsb::kDigitBits;
+      const int next = i + 1 < msd.size() ? msd[i + 1] * lsb::kDigitBits : -1;
+      begin_pass(c, shift);
+      lsb::OnesweepExtra x;
+      x.halves = r.os_halves;
+      LSB_TRY(onesweep_launch(c, r, shift, next, hist[i & 1], hist[(i + 1) & 1], x));
+      ++*passes;
+      if (i == 0) r.B = X2;  // A is X1 now
+    }
+    uint64_t pmask = 0;
+    for (int b : msd) pmask |= (uint64_t)(lsb::kBuckets - 1) << (b * lsb::kDigitBits);
+    Elem* const src = r.A;
+    Elem* const dst = msd.empty() ? X1 : r.B;
+    uint32_t* err = r.os_ctr + lsb::kOnesweepSubs + 1;
+    begin_pass(c, 64);
+    HIP_TRY(hipMemsetAsync(err, 0, sizeof(uint32_t), r.stream));
+    {
+      Timer t(c, &r, LSB_K_SEGSORT);
+      HIP_TRY(lsb::launch_segsort(src, dst, m, pmask, err, 3 * r.os_grid / 2, r.stream));
+    }
+    count_pass_elems(c, m);
+    ++*passes;
+    HIP_TRY(hipMemcpyAsync(r.os_err_h + 1, err, sizeof(uint32_t), hipMemcpyDeviceToHost, r.stream));
+    HIP_TRY(hipStreamSynchronize(r.stream));
+    if (r.os_err_h[1] == 0) {
+      r.A = dst;
+      r.B = src;
+      r.R = (X0 != dst && X0 != src) ? X0 : (X1 != dst && X1 != src) ? X1 : X2;
+    } else {  // a segment too long for k_segsort: the LSD passes over the kept input
+      r.A = X0;
+      r.B = X1;
+      r.R = X2;
+      counted = -1;
+      if (!digits.empty()) LSB_TRY(first_hist(digits[0], &skewed));
+      LSB_TRY(onesweep_digits(c, r, digits, passes));
+    }
   }
   // The look-back's give-up word, read by lsb_sync.
   HIP_TRY(hipMemcpyAsync(r.os_err_h, r.os_ctr + lsb::kOnesweepSubs, sizeof(uint32_t),
@@ -1849,6 +1994,10 @@ int lsb_set_option(lsb_ctx_t* c, int option, int64_t value) {
     case LSB_OPT_EXCHANGE_SELF:
       c->self_coll = value != 0;
       return LSB_OK;
+    case LSB_OPT_HYBRID:
+      if (value < 0 || value > 1) return fail(LSB_ERR_INVALID, "lsb_set_option", "hybrid must be 0 or 1");
+      c->hybrid = value != 0;
+      return LSB_OK;
     case LSB_OPT_ONESWEEP_SPLIT:
       if (value < 0 || value > 2) return fail(LSB_ERR_INVALID, "lsb_set_option", "split must be 0..2");
       c->os_split = (int)value;
@@ -2090,13 +2239,14 @@ int lsb_get_pass_stats(lsb_ctx_t* c, int pass, int* shift, int64_t* launches, in
   LSB_TRY(check_ctx(c));
   if (pass < 0 || pass >= LSB_MAX_PASSES) return fail(LSB_ERR_INVALID, "lsb_get_pass_stats", "pass");
   LSB_TRY(resolve_timing(c));
-  const bool ran = c->pass_launches[pass][LSB_K_SCATTER] > 0;
-  if (shift) *shift = ran ? c->pass_shift[pass] : -1;
-  if (launches) *launches = c->pass_launches[pass][LSB_K_SCATTER];
+  // The pass's sorting kernel: k_onesweep / k_scatter, or k_segsort (shift 64).
+  const int64_t sorts = c->pass_launches[pass][LSB_K_SCATTER] + c->pass_launches[pass][LSB_K_SEGSORT];
+  if (shift) *shift = sorts > 0 ? c->pass_shift[pass] : -1;
+  if (launches) *launches = sorts;
   if (elems) *elems = c->pass_elems[pass];
   // The count kernels: k_subhist / k_upsweep (read) and k_scan.
   if (ms_count) *ms_count = c->pass_ms[pass][LSB_K_UPSWEEP] + c->pass_ms[pass][LSB_K_SCAN];
-  if (ms_scatter) *ms_scatter = c->pass_ms[pass][LSB_K_SCATTER];
+  if (ms_scatter) *ms_scatter = c->pass_ms[pass][LSB_K_SCATTER] + c->pass_ms[pass][LSB_K_SEGSORT];
   if (ms_exchange) *ms_exchange = c->pass_ms[pass][LSB_K_EXCHANGE];
   if (ms_place) *ms_place = c->pass_ms[pass][LSB_K_PLACE];
   return LSB_OK;

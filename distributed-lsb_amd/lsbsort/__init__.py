@@ -43,13 +43,14 @@ UNIQUE_ID_BYTES = 128
 LSB_OK = 0
 LSB_ERR_VERIFY = 5
 DIST_UNIFORM, DIST_ZIPF = 0, 1
-K_UPSWEEP, K_SCAN, K_SCATTER, K_EXCHANGE, K_PLACE, K_SORT = range(6)
-KERNEL_NAMES = ("upsweep", "scan", "scatter", "exchange", "place", "sort")
+K_UPSWEEP, K_SCAN, K_SCATTER, K_EXCHANGE, K_PLACE, K_SORT, K_SEGSORT = range(7)
+KERNEL_NAMES = ("upsweep", "scan", "scatter", "exchange", "place", "sort", "segsort")
 OPT_TIMING, OPT_FORCE_EXCHANGE, OPT_SKIP_CONSTANT_DIGITS, OPT_EXCHANGE_SLICES, OPT_EXCHANGE_P2P = 0, 1, 2, 3, 4
 OPT_EXCHANGE_PEER = 5
 OPT_ONESWEEP = 6
 OPT_EXCHANGE_SELF = 7
 OPT_ONESWEEP_SPLIT = 8
+OPT_HYBRID = 9
 MAX_PASSES = 16
 
 
@@ -199,7 +200,7 @@ def source_digest() -> str:
     order the Makefile hashes them (SOURCES)."""
     import hashlib
     h = hashlib.sha256()
-    for rel in ("csrc/lsb_kernels.hip", "csrc/lsb_merge.hip", "csrc/lsb_runtime.cpp",
+    for rel in ("csrc/lsb_kernels.hip", "csrc/lsb_merge.hip", "csrc/lsb_segsort.hip", "csrc/lsb_runtime.cpp",
                 "csrc/lsb_kernels.h", "../include/lsb.h"):
         with open(os.path.join(ROOT_DIR, rel), "rb") as f:
             h.update(f.read())

@@ -65,7 +65,8 @@ typedef struct lsb_ctx lsb_ctx_t;
 #define LSB_K_EXCHANGE  3  /* bucket-count allgather + element all-to-all */
 #define LSB_K_PLACE     4  /* received runs -> final local slots          */
 #define LSB_K_SORT      5  /* whole lsb_sort()                            */
-#define LSB_K_COUNT     6
+#define LSB_K_SEGSORT   6  /* segmented local sort (LSB_OPT_HYBRID)       */
+#define LSB_K_COUNT     7
 
 /* Options for lsb_set_option(). */
 #define LSB_OPT_TIMING          0  /* 1: record HIP events around every kernel */
@@ -99,6 +100,17 @@ typedef struct lsb_ctx lsb_ctx_t;
                                       1/32 of a rank's records: the tile is staged in two
                                       halves, 3 workgroups per CU); 1 never split; 2 always
                                       split.  Same output. */
+#define LSB_OPT_HYBRID          9  /* local sorts without an exchange between digits (P == 1,
+                                      and each rank's block in the whole-key form): 0 (default)
+                                      the LSD passes; 1 the hybrid: stable 8-bit passes on the k
+                                      most significant varying bytes only (k = 4 at 2^30 records),
+                                      then ONE segmented local sort (k_segsort) orders every run
+                                      of records equal on those bytes by the whole key.  Same
+                                      output (the stable sort by key) from k + 1 passes over HBM
+                                      instead of up to 8.  Skewed keys (one bucket of the first
+                                      byte over 1/32 of the records) take the LSD passes; a
+                                      segment longer than 1024 records makes the sort redo the
+                                      kept input by the LSD passes.  Needs a third buffer. */
 
 /* ---- geometry: DistributedArray::create (mpi/mpi_lsbsort.cpp:144-149) ---- */
 int64_t lsb_per_rank(int64_t n_total, int num_ranks);            /* ceil(n/P) */

@@ -1,0 +1,161 @@
+"""Hybrid local sort (LSB_OPT_HYBRID): k stable k_onesweep passes on the
+most significant varying bytes, then k_segsort orders every segment (run of
+records equal on those bytes) by the whole key.
+
+The output must be the reference's: the stable sort by key
+(mpi/mpi_lsbsort.cpp:580-585 produces it by LSD passes; the verify at
+:722-737 checks exactly that), bit for bit against the oracle.  Sizes straddle
+k_segsort's 4096-record tiles and the choice of k; distributions include the
+skewed ones that take the LSD passes directly, and keys whose segments run
+past k_segsort's 1024-record limit, where the sort must redo the kept input
+with the LSD passes.
+"""
+import numpy as np
+import pytest
+
+from test_gpu_sort import DT, _dist
+
+pytestmark = pytest.mark.gpu
+
+T = 4096
+
+
+def _sort(lsbsort, a, skip=1, split=0, timing=False):
+    with lsbsort.World(a.size, ranks=1) as w:
+        w.set_option(lsbsort.OPT_HYBRID, 1)
+        w.set_option(lsbsort.OPT_SKIP_CONSTANT_DIGITS, skip)
+        w.set_option(lsbsort.OPT_ONESWEEP_SPLIT, split)
+        w.set_timing(timing)
+        w.copy_in(0, a)
+        w.my_sort()
+        w.sync()
+        return w.copy_out(0), w.last_sort(), (w.pass_stats() if timing else None)
+
+
+def _uniform(n, seed):
+    rng = np.random.default_rng(seed)
+    a = np.zeros(n, dtype=DT)
+    a["key"] = rng.integers(0, 2**64 - 1, n, dtype=np.uint64)
+    a["val"] = np.arange(n, dtype=np.uint64)
+    return a
+
+
+@pytest.mark.parametrize("n", [1, 2, 100, 128, 129, 1000, T - 1, T, T + 1, 2 * T + 3, 10_000, 65_537,
+                               1 << 20, (1 << 20) + 12_345, 1 << 22])
+def test_sizes_bit_exact(lsb_built, oracle_mod, n):
+    a = _uniform(n, n)
+    out, (lp, ex, _), _ = _sort(lsb_built, a)
+    assert np.array_equal(out, oracle_mod.stable_sort(a))
+    # k MSD passes + one segmented sort: fewer passes than the 8 LSD ones
+    # (tiny blocks look skewed to the 1/32 rule and take the LSD passes)
+    assert ex == 0 and (lp <= 5 or n < 1000), lp
+
+
+@pytest.mark.parametrize("n,k", [(256, 1), (257, 2), (1000, 2), (1 << 16, 2), (1 << 22, 3),
+                                 ((1 << 24) + 1, 4)])
+def test_msd_byte_count(lsb_built, oracle_mod, n, k):
+    """k = the fewest top bytes whose varying bits reach ceil(log2 n);
+    the per-pass stats show the k byte passes (top bytes, least significant
+    first) and the segmented sort (shift 64)."""
+    a = _uniform(n, 7 * n)
+    out, (lp, _, _), rows = _sort(lsb_built, a, timing=True)
+    assert np.array_equal(out, oracle_mod.stable_sort(a))
+    assert lp == k + 1
+    assert [r["shift"] for r in rows] == [8 * (8 - k + i) for i in range(k)] + [64]
+    assert all(r["elems"] == n for r in rows)
+
+
+@pytest.mark.parametrize("name", ["all_equal", "two_keys", "hot_bucket", "high_bits_only",
+                                  "zipf", "sorted", "reverse", "small_range"])
+@pytest.mark.parametrize("n", [200_003, 1 << 21])
+def test_distributions_bit_exact(lsb_built, oracle_mod, name, n):
+    rng = np.random.default_rng(hash((name, n)) & 0xFFFF)
+    a = _dist(name, n, rng)
+    out, _, _ = _sort(lsb_built, a)
+    assert np.array_equal(out, oracle_mod.stable_sort(a))
+
+
+@pytest.mark.parametrize("split", [1, 2])
+def test_stage_split_forced(lsb_built, oracle_mod, split):
+    a = _uniform(300_001, split)
+    out, _, _ = _sort(lsb_built, a, split=split)
+    assert np.array_equal(out, oracle_mod.stable_sort(a))
+
+
+def test_skip_constant_digits_off(lsb_built, oracle_mod):
+    a = _uniform(500_009, 3)
+    out, (lp, _, _), _ = _sort(lsb_built, a, skip=0)
+    assert np.array_equal(out, oracle_mod.stable_sort(a))
+    assert lp == 4  # 3 top bytes (guessed from n alone) + the segmented sort
+
+
+def test_duplicate_keys_keep_input_order(lsb_built, oracle_mod):
+    """Equal keys share a segment; k_segsort ranks them by input position."""
+    rng = np.random.default_rng(11)
+    n = 1 << 20
+    a = np.zeros(n, dtype=DT)
+    pool = rng.integers(0, 2**64 - 1, n // 8, dtype=np.uint64)
+    a["key"] = pool[rng.integers(0, pool.size, n)]
+    a["val"] = np.arange(n, dtype=np.uint64)
+    out, _, _ = _sort(lsb_built, a)
+    assert np.array_equal(out, oracle_mod.stable_sort(a))
+
+
+@pytest.mark.parametrize("bases", [1024, 4096])
+def test_long_segments_fall_back_to_lsd(lsb_built, oracle_mod, bases):
+    """n / bases records share each of `bases` random top parts: the first
+    byte looks uniform (no skew), but segments hold ~1024-4096 records, past
+    k_segsort's limit, so the sort redoes the kept input by the LSD passes."""
+    rng = np.random.default_rng(bases)
+    n = 1 << 22
+    top = rng.integers(0, 2**64 - 1, bases, dtype=np.uint64) & np.uint64(0xFFFFFFFFFF000000)
+    a = np.zeros(n, dtype=DT)
+    a["key"] = top[rng.integers(0, bases, n)] | rng.integers(0, 1 << 24, n, dtype=np.uint64)
+    a["val"] = np.arange(n, dtype=np.uint64)
+    out, (lp, _, _), _ = _sort(lsb_built, a)
+    assert np.array_equal(out, oracle_mod.stable_sort(a))
+    assert lp == 3 + 1 + 8  # 3 byte passes + the failed segmented sort + the LSD passes
+
+
+def test_generated_input_verifies(lsb_built, digests, oracle_mod):
+    for row in digests["rows"]:
+        if row["P"] != 1:
+            continue
+        with lsb_built.World(row["n"], ranks=1) as w:
+            w.set_option(lsb_built.OPT_HYBRID, 1)
+            w.generate()
+            w.my_sort()
+            assert oracle_mod.digest(w.copy_out(0)) == row["output"]
+            assert w.verify() == (True, -1)
+
+
+def test_repeated_sorts_on_one_context(lsb_built, oracle_mod):
+    """The hybrid rotates three buffers; the look-back status rows are
+    shared with the LSD passes of the same context."""
+    n = 300_007
+    with lsb_built.World(n, ranks=1) as w:
+        for i in range(4):
+            w.set_option(lsb_built.OPT_HYBRID, i % 2)
+            a = _uniform(n, 100 + i)
+            w.copy_in(0, a)
+            w.my_sort()
+            assert np.array_equal(w.copy_out(0), oracle_mod.stable_sort(a))
+
+
+@pytest.mark.parametrize("P", [2, 4, 8])
+def test_whole_key_local_sorts(lsb_built, oracle_mod, digests, P):
+    """Each rank's local sort of the whole-key exchange (radix_bits = 64)."""
+    for row in digests["rows"]:
+        if row["P"] != P:
+            continue
+        with lsb_built.World(row["n"], ranks=P, radix_bits=64) as w:
+            w.set_option(lsb_built.OPT_HYBRID, 1)
+            w.generate()
+            w.my_sort()
+            assert oracle_mod.digest(w.gather_global()) == row["output"]
+
+
+def test_option_range(lsb_built):
+    with lsb_built.World(10, ranks=1) as w:
+        with pytest.raises(lsb_built.LsbError):
+            w.set_option(lsb_built.OPT_HYBRID, 2)

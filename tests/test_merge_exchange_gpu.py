@@ -93,7 +93,7 @@ def test_reduce_scan_local_sort(lsb_built, oracle_mod, digests, P):
     assert np.array_equal(out, oracle_mod.stable_sort(a))
 
 
-@pytest.mark.parametrize("mask,passes", [(0x00000000FFFFFFFF, 4), (0xFF000000000000FF, 2), (0, 1)])
+@pytest.mark.parametrize("mask,passes", [(0x00000000FFFFFFFF, 4), (0xFF000000000000FF, 2), (0, 0)])
 def test_constant_digits_skipped_locally(lsb_built, oracle_mod, mask, passes):
     n, P = 100_003, 3
     rng = np.random.default_rng(mask & 0xFFFF)
