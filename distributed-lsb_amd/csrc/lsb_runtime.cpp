@@ -251,10 +251,11 @@ void begin_pass(lsb_ctx* c, int shift) {
   if (c->cur_pass < LSB_MAX_PASSES) c->pass_shift[c->cur_pass] = shift;
 }
 
-// Records one local pass of m records processed (the scatter kernel's elements).
-void count_pass_elems(lsb_ctx* c, int64_t m) {
+// Records one local pass of m records processed (lsb_get_pass_stats); a
+// scatter kernel's records also go to lsb_get_scatter_elems.
+void count_pass_elems(lsb_ctx* c, int64_t m, bool scatter = true) {
   if (!c->timing) return;
-  c->scatter_elems += m;
+  if (scatter) c->scatter_elems += m;
   if (c->cur_pass >= 0 && c->cur_pass < LSB_MAX_PASSES) c->pass_elems[c->cur_pass] += m;
 }
 
@@ -1154,7 +1155,7 @@ int sort_hybrid_rank(lsb_ctx* c, Rank& r, int* passes, uint64_t* varying) {
       Timer t(c, &r, LSB_K_SEGSORT);
       HIP_TRY(lsb::launch_segsort(src, dst, m, pmask, err, 3 * r.os_grid / 2, r.stream));
     }
-    count_pass_elems(c, m);
+    count_pass_elems(c, m, false);
     ++*passes;
     HIP_TRY(hipMemcpyAsync(r.os_err_h + 1, err, sizeof(uint32_t), hipMemcpyDeviceToHost, r.stream));
     HIP_TRY(hipStreamSynchronize(r.stream));

@@ -344,7 +344,7 @@ def test_error_codes_on_a_context(lsb_built):
         assert lib.lsb_set_option(h, 99, 1) == 1
         assert lib.lsb_generate_ex(h, 7, 0.0) == 1
         assert lib.lsb_generate_ex(h, lsb_built.DIST_ZIPF, 0.0) == 1
-        assert lib.lsb_get_kernel_stats(h, 6, None, None) == 1
+        assert lib.lsb_get_kernel_stats(h, 7, None, None) == 1
         first, num = ctypes.c_int(), ctypes.c_int()
         assert lib.lsb_local_ranks(h, ctypes.byref(first), ctypes.byref(num)) == 0
         assert (first.value, num.value) == (0, 2)

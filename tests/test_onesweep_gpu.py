@@ -45,7 +45,9 @@ def test_sizes_bit_exact(lsb_built, oracle_mod, n):
     assert np.array_equal(out, oracle_mod.stable_sort(a))
     ref, last0 = _sort(lsb_built, a, 0)
     assert np.array_equal(out, ref)
-    assert last == last0
+    # reduce-then-scan always runs digit 0 (its count kernel reads the span);
+    # single-read passes skip it too when it is constant (n = 1: every digit)
+    assert last == last0 or (n == 1 and last == (0, 0, 0) and last0 == (1, 0, 0))
 
 
 @pytest.mark.parametrize("name", ["all_equal", "two_keys", "hot_bucket", "high_bits_only",

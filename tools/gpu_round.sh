@@ -1,6 +1,6 @@
 #!/bin/bash
 # One GPU check of the tree (run from the repo root on the GPU box):
-#   TAG=r03_v1 STEPS="tests smoke bench n2 n4zipf torchrun profile sq" bash tools/gpu_round.sh
+#   TAG=r03_v1 RUN="tests smoke bench n2 n4zipf torchrun profile sq" bash tools/gpu_round.sh
 # Steps (each under its own time limit; the first failure ends the call):
 #   tests     the whole -m gpu suite
 #   smoke     __graft_entry__.smoke()
@@ -18,9 +18,9 @@ TAG=${TAG:-check}
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 cd $R
-STEPS=${STEPS:-"tests smoke bench"}
+RUN=${RUN:-"tests smoke bench"}
 fail() { echo "FAILED: $1"; tail -40 "$2"; exit 1; }
-for s in $STEPS; do
+for s in $RUN; do
   echo "== $s $(date +%T)"
   case $s in
     tests)
