@@ -358,7 +358,8 @@ def parallelism(N, radix, a):
         return (f"{N} ranks, RCCL between ranks sharing GPUs over its socket transport "
                 f"(rehearsal of the RCCL path, not a measurement)")
     if radix == 64:
-        return (f"block partition over {N} GPUs; local sort per GPU, splitter search (8 RCCL AllGathers "
+        return (f"block partition over {N} GPUs; local sort per GPU" +
+                (" (hybrid)" if a.passes == "hybrid" else "") + ", splitter search (8 RCCL AllGathers "
                 f"of candidate counts), one RCCL " + ("AllToAllv" if a.exchange == "alltoallv" else
                                                        "grouped Send/Recv") +
                 ", stable merge tree of the P runs")
@@ -520,8 +521,10 @@ def extra_argv(a, flags, steps=3):
 
 def whole_key_argv(a):
     """The whole-key extra: the 64-bit exchange digit (a per-digit --exchange
-    peer becomes AllToAllv)."""
-    return extra_argv(a, ["--radix-bits", "64"] + (["--exchange", "alltoallv"] if a.exchange == "peer" else []))
+    peer becomes AllToAllv), each rank's local sort by the hybrid (the
+    fastest local sort; same output) unless --passes chose another form."""
+    return extra_argv(a, ["--radix-bits", "64"] + (["--exchange", "alltoallv"] if a.exchange == "peer" else []) +
+                      (["--passes", "hybrid"] if a.passes == "onesweep" else []))
 
 
 def merge_extra(out, name, ok, text, report):

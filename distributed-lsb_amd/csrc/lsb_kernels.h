@@ -120,10 +120,31 @@ hipError_t onesweep_profile(unsigned long long* out10, bool reset);
 // forms, P > 1): totals[b] = the pass's 256 digit counts; count16 (zeroed
 // here) = the 65536 counts of the 16-bit digit at shift - 8, for the high
 // byte of a 16-bit exchange digit whose input is sorted by the low byte.
+// The hybrid's last byte pass (LSB_OPT_HYBRID, lsb_segsort.hip): the pass
+// also orders every segment (records equal on pmask, the k top varying
+// bytes) inside its tile by the whole key, so no separate k_segsort pass is
+// needed.  A segment lies inside one run of records equal on rmask (pmask
+// without this pass's byte), and the pass's input is sorted by rmask; only
+// runs that cross a tile boundary can leave a segment split between two
+// tiles.  For those the pass records the output slot of every record of its
+// first and last run (pos[tile][0][i]: record i of the last run, pos[tile]
+// [1][i]: record i of the first run, input order; meta[tile][0..1] = their
+// counts, 0 when the run does not cross), and launch_segfix merges the
+// split segments.  *err |= 1 when a run holds more than kSegCap records or a
+// segment more than kSegMax (the runtime then runs k_segsort on the output).
+constexpr int kSegCap = 512;
+struct SegPass {
+  uint64_t pmask = 0;
+  uint64_t rmask = 0;
+  int64_t* pos = nullptr;
+  uint32_t* meta = nullptr;
+  uint32_t* err = nullptr;
+};
 struct OnesweepExtra {
   uint64_t* totals = nullptr;
   uint64_t* count16 = nullptr;
   int halves = 1;  // 2: split stage, 3 workgroups per CU (skewed keys; not with count16)
+  const SegPass* seg = nullptr;  // the hybrid's last pass (no next digit, whole stage)
 };
 // The runtime's choice of OnesweepExtra::halves for a rank, from a digit's
 // sub-array histogram (kOnesweepSubs x 256 counts of m records): 2 when one
@@ -143,6 +164,10 @@ hipError_t launch_onesweep(const Elem* in, Elem* out, int64_t m, int shift, int 
 constexpr int kSegMax = 1024;
 hipError_t launch_segsort(const Elem* in, Elem* out, int64_t m, uint64_t pmask, uint32_t* err,
                           int grid, hipStream_t s);
+// After a SegPass launch over m records on the byte at `shift`: merge every
+// segment split between tiles t and t + 1 (both tiles' crossing runs, from
+// seg.pos / seg.meta), in place in `out`.
+hipError_t launch_segfix(Elem* out, int64_t m, int shift, const SegPass& seg, int grid, hipStream_t s);
 
 // Receiver-side placement of one source's received range: src[i] (receive
 // index k0 + i) goes to out[off_row[digit] + k0 + i], off_row = the source's

@@ -760,15 +760,25 @@ __device__ unsigned long long g_os_prof[10];
 // this way (their serialised next-digit adds hide behind a third
 // workgroup); uniform keys 4.7 % slower (two more barriers per tile, half-
 // length write phases): profiles/ab/r02_ab12_*.
-template <int BLOCK, int IPT, bool NEXT, bool C16, int HALVES>
+//
+// SEG (the hybrid's last pass, SegPass in lsb_kernels.h): the write-out also
+// orders each segment (records equal on seg.pmask; inside the tile they are
+// adjacent in the stage, in one bucket run) by the whole key: a record's slot
+// in its run is its segment's first slot + #(segment keys < mine) + #(equal
+// keys staged before me), found by walking its stage neighbours (segments
+// hold ~0.25 records on average at the runtime's choice of bytes).  The
+// records of the tile's first and last rmask runs, when those cross the tile
+// boundary, report their output slots for launch_segfix.
+template <int BLOCK, int IPT, bool NEXT, bool C16, int HALVES, bool SEG = false>
 __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_onesweep(
     const Elem* __restrict__ in, Elem* __restrict__ out, int64_t m, int shift, int next_shift,
     const uint32_t* __restrict__ sub_hist, uint32_t* __restrict__ next_hist,
     uint32_t* __restrict__ status, uint32_t* __restrict__ tile_ctr, uint32_t epoch,
     uint32_t* __restrict__ err, uint64_t* __restrict__ totals,
-    unsigned long long* __restrict__ count16) {
+    unsigned long long* __restrict__ count16, SegPass seg) {
   constexpr int W = BLOCK / 64;
   constexpr int T = BLOCK * IPT;
+  static_assert(!SEG || (!NEXT && !C16 && HALVES == 1), "the segment pass: last pass, whole stage");
   // Thread t < 256 owns bucket t (counts, scan, look-back, offsets); with
   // BLOCK = 512 the other threads only load, rank, stage and write.
   static_assert(BLOCK % kBuckets == 0, "bucket threads");
@@ -786,6 +796,8 @@ __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_
   __shared__ uint32_t scan32[W];
   __shared__ int32_t s_tile, s_sub;
   __shared__ uint32_t tile_lo[2];  // C16: low byte of the tile's first, last record
+  __shared__ uint16_t org[SEG ? HT : 1];  // SEG: tile-local input index of each staged record
+  __shared__ int32_t s_rl, s_rf;          // SEG: first index of the last run, end of the first
 
   const int t = threadIdx.x;
   const bool bkt = BLOCK == kBuckets || t < kBuckets;  // a bucket thread
@@ -863,6 +875,10 @@ __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_
     if (t == 0) {
       s_tile = nxt_tile;
       s_sub = nxt_sub;
+      if (SEG) {
+        s_rl = T;
+        s_rf = 0;
+      }
     }
 #pragma unroll
     for (int j = 0; j < kBuckets / 64; ++j) wcnt[w][lane + 64 * j] = 0;
@@ -888,6 +904,16 @@ __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_
     for (int i = 0; i < IPT; ++i) {
       const int li = wbase + i * 64;
       e[i] = li < nvalid ? load_elem_nt(in + tb + li) : Elem{0ull, 0ull};
+    }
+    // SEG: the rmask runs at the tile's two ends, and whether they cross.
+    uint64_t run_f = 0, run_l = 0;
+    bool cross_f = false, cross_l = false;
+    if (SEG) {
+      const uint64_t* keys = reinterpret_cast<const uint64_t*>(in);
+      run_f = keys[2 * tb] & seg.rmask;
+      run_l = keys[2 * (tb + nvalid - 1)] & seg.rmask;
+      cross_f = tb > 0 && (keys[2 * (tb - 1)] & seg.rmask) == run_f;
+      cross_l = tb + nvalid < m && (keys[2 * (tb + nvalid)] & seg.rmask) == run_l;
     }
 #ifdef LSB_OS_PROFILE
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -930,6 +956,12 @@ __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_
       const uint32_t pre = wcnt[w][d];
       rk[i] = pre + below;
       if (valid && below == 0) wcnt[w][d] = (WC)(pre + (uint32_t)__popcll(mt));
+      if (SEG && valid) {
+        const uint64_t rk_ = e[i].key & seg.rmask;
+        const int li = wbase + i * 64;
+        if (cross_l && rk_ == run_l) atomicMin(&s_rl, li);
+        if (cross_f && rk_ == run_f) atomicMax(&s_rf, li + 1);
+      }
       if (C16) {
         const int li = wbase + i * 64;
         if (li == 0) tile_lo[0] = (uint32_t)(e[i].key >> shift16) & 0xFFu;
@@ -983,6 +1015,7 @@ __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_
           const uint32_t d = (uint32_t)(e[i].key >> shift) & (kBuckets - 1);
           if (HALVES == 1) {
             stage[wcnt[w][d] + rk[i]] = e[i];
+            if (SEG) org[wcnt[w][d] + rk[i]] = (uint16_t)(wbase + i * 64);
           } else {
             if (h == 0) rk[i] += wcnt[w][d];
             if ((int)(rk[i] / HT) == h) stage[rk[i] - h * HT] = e[i];
@@ -1058,6 +1091,22 @@ __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_
 #endif
     if (t == 0) grab(nxt_tile, nxt_sub);  // in flight during the writes
 
+    // SEG: the crossing runs' records report their slots (none past kSegCap:
+    // *seg.err, and k_segsort orders the output instead).
+    int rl = nvalid, rf = 0;
+    if (SEG) {
+      const int nl = cross_l ? nvalid - s_rl : 0, nr = cross_f ? s_rf : 0;
+      const bool over = nl > kSegCap || nr > kSegCap;
+      if (t == 0) {
+        seg.meta[2 * (int64_t)tile] = over ? 0u : (uint32_t)nl;
+        seg.meta[2 * (int64_t)tile + 1] = over ? 0u : (uint32_t)nr;
+        if (over) atomicOr(seg.err, 1u);
+      }
+      if (!over) {
+        rl = nvalid - nl;
+        rf = nr;
+      }
+    }
     // The loop is instantiated twice (the launch-uniform `skewed` picks one
     // outside it): a per-record branch on it cost uniform keys 2.4 %.
     auto write_out = [&](auto skew_tag, int h) {
@@ -1066,13 +1115,47 @@ __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_
       for (int j = h * HT + t; j < jend; j += BLOCK) {
         const Elem v = stage[j - h * HT];
         const uint32_t d = (uint32_t)(v.key >> shift) & (kBuckets - 1);
-        const int64_t g = delta[d] + j;
+        int pos = j;
+        if (SEG) {
+          // The segment's neighbours in the stage (bounded: kSegMax).
+          const uint64_t pk = v.key & seg.pmask;
+          uint32_t less = 0, eqb = 0;
+          int k = j - 1;
+          const int klo = j - kSegMax > 0 ? j - kSegMax : 0;
+          while (k >= klo) {
+            const uint64_t kk = stage[k].key;
+            if ((kk & seg.pmask) != pk) break;
+            less += kk < v.key ? 1u : 0u;
+            eqb += kk == v.key ? 1u : 0u;
+            --k;
+          }
+          const int first = k + 1;
+          // kSegMax records walked without leaving the segment: too long
+          bool too_long = k < klo && klo > 0;
+          const int khi = j + 1 + kSegMax < nvalid ? j + 1 + kSegMax : nvalid;
+          k = j + 1;
+          while (k < khi) {
+            const uint64_t kk = stage[k].key;
+            if ((kk & seg.pmask) != pk) break;
+            less += kk < v.key ? 1u : 0u;
+            ++k;
+          }
+          too_long |= k == khi && khi < nvalid;
+          if (too_long) atomicOr(seg.err, 1u);
+          pos = first + (int)(less + eqb);
+        }
+        const int64_t g = delta[d] + pos;
         LSB_DASSERT(g >= 0 && g < m);
         // In range by construction.  The clamp keeps a look-back that gave up
         // (err set, output reported invalid) from storing outside `out`; a
         // clamp, not a branch: the conditional store cost 6 % of the sort.
         const uint64_t gs = (uint64_t)g < (uint64_t)(m - 1) ? (uint64_t)g : (uint64_t)(m - 1);
         store_elem(out + gs, v);
+        if (SEG) {
+          const int li = org[j];
+          if (li >= rl) seg.pos[(2 * (int64_t)tile) * kSegCap + (li - rl)] = (int64_t)gs;
+          if (li < rf) seg.pos[(2 * (int64_t)tile + 1) * kSegCap + li] = (int64_t)gs;
+        }
         if (NEXT) {
           const uint32_t c = cut[d];
           const uint32_t xs = (uint32_t)j >= (c & 0xFFFFu) ? (c >> 24) : ((c >> 16) & 0xFFu);
@@ -1683,31 +1766,39 @@ hipError_t launch_onesweep(const Elem* in, Elem* out, int64_t m, int shift, int 
   if (g > (TT + kSub - 1) / kSub * kSub) g = (TT + kSub - 1) / kSub * kSub;
   const dim3 gd((unsigned)g), bd(split ? kOsSplitBlock : kOsBlock);
   uint32_t* st = status;
-  if (c16) {
+  if (extra.seg) {
+    // The hybrid's last pass: no next digit, no 16-bit counts, whole stage.
+    if (next_shift >= 0 || c16 || extra.halves != 1 || !extra.seg->pos || !extra.seg->meta ||
+        !extra.seg->err)
+      return hipErrorInvalidValue;
+    hipLaunchKernelGGL((k_onesweep<kOsBlock, kOsIpt, false, false, 1, true>), gd, bd, 0, s, in, out, m,
+                       shift, 0, sub_hist, nullptr, st, tile_ctr, epoch, err, extra.totals, nullptr,
+                       *extra.seg);
+  } else if (c16) {
     // The 16-bit counts need the low byte below this digit, and no next
     // digit: the exchange follows this pass.
     if (shift < 8 || next_shift >= 0) return hipErrorInvalidValue;
     e = hipMemsetAsync(c16, 0, sizeof(uint64_t) * 65536, s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((k_onesweep<kOsBlock, kOsIpt, false, true, 1>), gd, bd, 0, s, in, out,
-                       m, shift, 0, sub_hist, nullptr, st, tile_ctr, epoch, err, extra.totals, c16);
+                       m, shift, 0, sub_hist, nullptr, st, tile_ctr, epoch, err, extra.totals, c16, SegPass());
   } else if (next_shift >= 0) {
     e = hipMemsetAsync(next_hist, 0, sizeof(uint32_t) * kSub * kBuckets, s);
     if (e != hipSuccess) return e;
     if (split)
       hipLaunchKernelGGL((k_onesweep<kOsSplitBlock, kOsSplitIpt, true, false, 2>), gd, bd, 0, s, in, out,
                          m, shift, next_shift, sub_hist, next_hist, st, tile_ctr, epoch, err,
-                         extra.totals, nullptr);
+                         extra.totals, nullptr, SegPass());
     else
       hipLaunchKernelGGL((k_onesweep<kOsBlock, kOsIpt, true, false, 1>), gd, bd, 0, s, in, out,
                          m, shift, next_shift, sub_hist, next_hist, st, tile_ctr, epoch, err,
-                         extra.totals, nullptr);
+                         extra.totals, nullptr, SegPass());
   } else if (split) {
     hipLaunchKernelGGL((k_onesweep<kOsSplitBlock, kOsSplitIpt, false, false, 2>), gd, bd, 0, s, in, out,
-                       m, shift, 0, sub_hist, nullptr, st, tile_ctr, epoch, err, extra.totals, nullptr);
+                       m, shift, 0, sub_hist, nullptr, st, tile_ctr, epoch, err, extra.totals, nullptr, SegPass());
   } else {
     hipLaunchKernelGGL((k_onesweep<kOsBlock, kOsIpt, false, false, 1>), gd, bd, 0, s, in, out,
-                       m, shift, 0, sub_hist, nullptr, st, tile_ctr, epoch, err, extra.totals, nullptr);
+                       m, shift, 0, sub_hist, nullptr, st, tile_ctr, epoch, err, extra.totals, nullptr, SegPass());
   }
   return hipGetLastError();
 }

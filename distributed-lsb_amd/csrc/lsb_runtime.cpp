@@ -97,6 +97,8 @@ struct Rank {
   int os_halves = 1;                    // this sort's k_onesweep stage split (1 or 2)
   uint32_t os_epoch = 0;                // last look-back epoch
   bool os_dirty = false;                // a launch failed: zero os_status before the next
+  int64_t* seg_pos = nullptr;           // [tiles][2][kSegCap] the hybrid's crossing-run slots
+  uint32_t* seg_meta = nullptr;         // [tiles][2] their counts
   int os_grid = 0;                      // persistent grid (2 workgroups per CU)
   // Per-digit exchange with single-read local passes (sort_exchange_onesweep):
   // os_hist[os_cur] is A's sub-array histogram of the byte at os_valid (-1:
@@ -144,7 +146,8 @@ struct lsb_ctx {
   bool onesweep = true;       // P == 1: single-read passes (k_subhist + k_onesweep)
   bool self_coll = false;     // the self segment also goes through the collective
   int os_split = 0;           // LSB_OPT_ONESWEEP_SPLIT: 0 auto, 1 never, 2 always
-  bool hybrid = false;        // LSB_OPT_HYBRID: k MSD-byte passes + k_segsort
+  int hybrid = 0;             // LSB_OPT_HYBRID: 0 off, 1 k byte passes (the last one
+                              // ordering segments, + k_segfix), 2 the same + a k_segsort pass
   int64_t coll_calls = 0, coll_bytes = 0, coll_max = 0;  // element payload handed to the collective
   // What the last lsb_sort ran (lsb_get_last_sort).
   int last_local_passes = 0;
@@ -363,6 +366,8 @@ void free_rank(Rank& r) {
   (void)hipHostFree(r.split_h);
   (void)hipFree(r.merge_path);
   (void)hipFree(r.os_status);
+  (void)hipFree(r.seg_pos);
+  (void)hipFree(r.seg_meta);
   (void)hipFree(r.os_hist);
   (void)hipFree(r.os_ctr);
   (void)hipHostFree(r.os_err_h);
@@ -1129,10 +1134,29 @@ int sort_hybrid_rank(lsb_ctx* c, Rank& r, int* passes, uint64_t* varying) {
     if (!digits.empty()) LSB_TRY(first_hist(digits[0], &skewed));
     LSB_TRY(onesweep_digits(c, r, digits, passes));
   } else {
-    // The k passes: A -> B, then B <-> R; the input X0 is kept.
+    // The k passes: A -> B, then B <-> R; the input X0 is kept.  The last
+    // one also orders every segment inside its tile (SegPass) and k_segfix
+    // merges the segments split between tiles; LSB_OPT_HYBRID = 2, or the
+    // split stage, leaves the segments to a k_segsort pass instead.
     Elem* const X0 = r.A;
     Elem* const X1 = r.B;
     Elem* const X2 = r.R;
+    uint64_t pmask = 0;
+    for (int b : msd) pmask |= (uint64_t)(lsb::kBuckets - 1) << (b * lsb::kDigitBits);
+    uint32_t* err = r.os_ctr + lsb::kOnesweepSubs + 1;
+    const bool fuse = c->hybrid == 1 && r.os_halves == 1 && !msd.empty();
+    lsb::SegPass sp;
+    if (fuse) {
+      const size_t tiles = (size_t)lsb::onesweep_tiles(m);
+      if (!r.seg_pos) LSB_TRY(dev_alloc(&r.seg_pos, tiles * 2 * lsb::kSegCap));
+      if (!r.seg_meta) LSB_TRY(dev_alloc(&r.seg_meta, tiles * 2));
+      sp.pmask = pmask;
+      sp.rmask = pmask & ~((uint64_t)(lsb::kBuckets - 1) << (msd.back() * lsb::kDigitBits));
+      sp.pos = r.seg_pos;
+      sp.meta = r.seg_meta;
+      sp.err = err;
+    }
+    HIP_TRY(hipMemsetAsync(err, 0, sizeof(uint32_t), r.stream));
     uint32_t* hist[2] = {r.os_hist, r.os_hist + lsb::kOnesweepSubs * lsb::kBuckets};
     for (size_t i = 0; i < msd.size(); ++i) {
       const int shift = msd[i] * lsb::kDigitBits;
@@ -1140,30 +1164,49 @@ int sort_hybrid_rank(lsb_ctx* c, Rank& r, int* passes, uint64_t* varying) {
       begin_pass(c, shift);
       lsb::OnesweepExtra x;
       x.halves = r.os_halves;
+      if (fuse && i + 1 == msd.size()) x.seg = &sp;
       LSB_TRY(onesweep_launch(c, r, shift, next, hist[i & 1], hist[(i + 1) & 1], x));
       ++*passes;
       if (i == 0) r.B = X2;  // A is X1 now
     }
-    uint64_t pmask = 0;
-    for (int b : msd) pmask |= (uint64_t)(lsb::kBuckets - 1) << (b * lsb::kDigitBits);
-    Elem* const src = r.A;
-    Elem* const dst = msd.empty() ? X1 : r.B;
-    uint32_t* err = r.os_ctr + lsb::kOnesweepSubs + 1;
-    begin_pass(c, 64);
-    HIP_TRY(hipMemsetAsync(err, 0, sizeof(uint32_t), r.stream));
-    {
-      Timer t(c, &r, LSB_K_SEGSORT);
-      HIP_TRY(lsb::launch_segsort(src, dst, m, pmask, err, 3 * r.os_grid / 2, r.stream));
+    if (msd.empty()) r.B = X1;
+    auto sync_err = [&](uint32_t* v) -> int {
+      HIP_TRY(hipMemcpyAsync(r.os_err_h + 1, err, sizeof(uint32_t), hipMemcpyDeviceToHost, r.stream));
+      HIP_TRY(hipStreamSynchronize(r.stream));
+      *v = r.os_err_h[1];
+      return LSB_OK;
+    };
+    bool sorted = false;
+    if (fuse) {
+      {
+        Timer t(c, &r, LSB_K_SEGSORT);
+        HIP_TRY(lsb::launch_segfix(r.A, m, msd.back() * lsb::kDigitBits, sp, 2 * r.os_grid, r.stream));
+      }
+      uint32_t e = 0;
+      LSB_TRY(sync_err(&e));
+      sorted = e == 0;
     }
-    count_pass_elems(c, m, false);
-    ++*passes;
-    HIP_TRY(hipMemcpyAsync(r.os_err_h + 1, err, sizeof(uint32_t), hipMemcpyDeviceToHost, r.stream));
-    HIP_TRY(hipStreamSynchronize(r.stream));
-    if (r.os_err_h[1] == 0) {
-      r.A = dst;
-      r.B = src;
-      r.R = (X0 != dst && X0 != src) ? X0 : (X1 != dst && X1 != src) ? X1 : X2;
-    } else {  // a segment too long for k_segsort: the LSD passes over the kept input
+    if (!sorted) {
+      // k_segsort: r.A is stably sorted by pmask (the fused pass's segments
+      // too, in or out of order).
+      HIP_TRY(hipMemsetAsync(err, 0, sizeof(uint32_t), r.stream));
+      begin_pass(c, 64);
+      {
+        Timer t(c, &r, LSB_K_SEGSORT);
+        HIP_TRY(lsb::launch_segsort(r.A, r.B, m, pmask, err, 3 * r.os_grid / 2, r.stream));
+      }
+      count_pass_elems(c, m, false);
+      ++*passes;
+      uint32_t e = 0;
+      LSB_TRY(sync_err(&e));
+      if (e == 0) {
+        std::swap(r.A, r.B);
+        sorted = true;
+      }
+    }
+    if (sorted) {
+      r.R = (X0 != r.A && X0 != r.B) ? X0 : (X1 != r.A && X1 != r.B) ? X1 : X2;
+    } else {  // a segment too long for the segment sorts: the LSD passes over the kept input
       r.A = X0;
       r.B = X1;
       r.R = X2;
@@ -1996,8 +2039,8 @@ int lsb_set_option(lsb_ctx_t* c, int option, int64_t value) {
       c->self_coll = value != 0;
       return LSB_OK;
     case LSB_OPT_HYBRID:
-      if (value < 0 || value > 1) return fail(LSB_ERR_INVALID, "lsb_set_option", "hybrid must be 0 or 1");
-      c->hybrid = value != 0;
+      if (value < 0 || value > 2) return fail(LSB_ERR_INVALID, "lsb_set_option", "hybrid must be 0, 1 or 2");
+      c->hybrid = (int)value;
       return LSB_OK;
     case LSB_OPT_ONESWEEP_SPLIT:
       if (value < 0 || value > 2) return fail(LSB_ERR_INVALID, "lsb_set_option", "split must be 0..2");

@@ -46,7 +46,10 @@ __device__ __forceinline__ Elem seg_load_nt(const Elem* p) {
   return Elem{v.x, v.y};
 }
 
-__global__ __launch_bounds__(kSegBlock) __attribute__((amdgpu_waves_per_eu(6))) void k_segsort(const Elem* __restrict__ in,
+#ifndef LSB_SEG_WAVES
+#define LSB_SEG_WAVES 6  // waves per SIMD: 3 workgroups of 8 waves per CU
+#endif
+__global__ __launch_bounds__(kSegBlock) __attribute__((amdgpu_waves_per_eu(LSB_SEG_WAVES))) void k_segsort(const Elem* __restrict__ in,
                                                        Elem* __restrict__ out, int64_t m,
                                                        uint64_t pmask, uint32_t* __restrict__ err) {
   constexpr int T = kSegTile;
@@ -173,7 +176,12 @@ __global__ __launch_bounds__(kSegBlock) __attribute__((amdgpu_waves_per_eu(6))) 
       // In range by construction; the clamp keeps a record of an over-long
       // segment (output invalid, *err set) inside `out`.
       g = g < m ? g : m - 1;
+#ifdef LSB_SEG_NT_STORE
+      typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+      __builtin_nontemporal_store(u64x2{key, val}, reinterpret_cast<u64x2*>(out + g));
+#else
       *reinterpret_cast<ulonglong2*>(out + g) = make_ulonglong2(key, val);
+#endif
     };
     if (w0 < nvalid) {
 #pragma unroll
@@ -188,12 +196,106 @@ __global__ __launch_bounds__(kSegBlock) __attribute__((amdgpu_waves_per_eu(6))) 
   if (bad) atomicOr(err, 1u);
 }
 
+// k_segfix: after the hybrid's last pass with SegPass, the only segments
+// out of order are those split between two tiles: a segment lies inside
+// one rmask run, and only the run crossing the boundary between tiles t and
+// t + 1 has records on both sides.  Each side sorted its part in the stage
+// (k_onesweep SEG), and both parts sit in adjacent slots: the end of tile
+// t's bucket run, then the start of tile t + 1's.  One workgroup per
+// boundary gathers both crossing runs (slots from seg.pos), and for every
+// bucket present on both sides merges the two sorted parts, stably (tile t's
+// records first on equal keys), back into the same slots.
+constexpr int kFixBlock = 256;
+
+__global__ __launch_bounds__(kFixBlock) void k_segfix(Elem* __restrict__ out, int64_t m, int shift,
+                                                      int64_t TT, SegPass seg) {
+  __shared__ uint64_t lk[kSegCap], lv[kSegCap], rk[kSegCap], rv[kSegCap];
+  __shared__ int64_t lp[kSegCap], rp[kSegCap];
+  const int t = threadIdx.x;
+  for (int64_t b = blockIdx.x; b + 1 < TT; b += gridDim.x) {
+    const int nl = (int)seg.meta[2 * b];
+    const int nr = (int)seg.meta[2 * (b + 1) + 1];
+    if (nl == 0 || nr == 0) continue;  // the same for the whole workgroup
+    const int64_t* pl = seg.pos + (2 * b) * kSegCap;
+    const int64_t* pr = seg.pos + (2 * (b + 1) + 1) * kSegCap;
+    for (int i = t; i < nl; i += kFixBlock) {
+      int64_t q = pl[i];
+      q = q < 0 ? 0 : (q < m ? q : m - 1);
+      const Elem x = out[q];
+      lp[i] = q;
+      lk[i] = x.key;
+      lv[i] = x.val;
+    }
+    for (int i = t; i < nr; i += kFixBlock) {
+      int64_t q = pr[i];
+      q = q < 0 ? 0 : (q < m ? q : m - 1);
+      const Elem x = out[q];
+      rp[i] = q;
+      rk[i] = x.key;
+      rv[i] = x.val;
+    }
+    __syncthreads();
+    // New slot of each record of a bucket present on both sides: the
+    // bucket's first slot (its first record of tile t) + its rank on its
+    // own side (slot order = key order) + the other side's records before it.
+    constexpr int kPer = (2 * kSegCap + kFixBlock - 1) / kFixBlock;
+    int64_t dst[kPer];
+    int cnt = 0;
+    for (int x = t; x < nl + nr; x += kFixBlock, ++cnt) {
+      dst[cnt] = -1;
+      const bool left = x < nl;
+      const int i = left ? x : x - nl;
+      const uint64_t key = left ? lk[i] : rk[i];
+      const int64_t slot = left ? lp[i] : rp[i];
+      const uint32_t c = (uint32_t)(key >> shift) & (kBuckets - 1);
+      int64_t start = INT64_MAX;
+      int own = 0, other = 0, in_l = 0, in_r = 0;
+      for (int y = 0; y < nl; ++y) {
+        if (((uint32_t)(lk[y] >> shift) & (kBuckets - 1)) != c) continue;
+        ++in_l;
+        start = lp[y] < start ? lp[y] : start;
+        if (left) own += lp[y] < slot ? 1 : 0;
+        else other += lk[y] <= key ? 1 : 0;
+      }
+      for (int y = 0; y < nr; ++y) {
+        if (((uint32_t)(rk[y] >> shift) & (kBuckets - 1)) != c) continue;
+        ++in_r;
+        if (left) other += rk[y] < key ? 1 : 0;
+        else own += rp[y] < slot ? 1 : 0;
+      }
+      if (in_l > 0 && in_r > 0) dst[cnt] = start + own + other;
+    }
+    __syncthreads();  // every record is read before any is rewritten
+    cnt = 0;
+    for (int x = t; x < nl + nr; x += kFixBlock, ++cnt) {
+      if (dst[cnt] < 0 || dst[cnt] >= m) continue;
+      const bool left = x < nl;
+      const int i = left ? x : x - nl;
+      out[dst[cnt]] = left ? Elem{lk[i], lv[i]} : Elem{rk[i], rv[i]};
+    }
+    __syncthreads();  // lk ... rp are rewritten for the next boundary
+  }
+}
+
 }  // namespace
+
+hipError_t launch_segfix(Elem* out, int64_t m, int shift, const SegPass& seg, int grid, hipStream_t s) {
+  if (m <= 0) return hipSuccess;
+  const int64_t TT = (m + kTile - 1) / kTile;
+  if (TT < 2) return hipSuccess;
+  int64_t g = grid < 1 ? 1 : grid;
+  if (g > TT - 1) g = TT - 1;
+  hipLaunchKernelGGL(k_segfix, dim3((unsigned)g), dim3(kFixBlock), 0, s, out, m, shift, TT, seg);
+  return hipGetLastError();
+}
 
 hipError_t launch_segsort(const Elem* in, Elem* out, int64_t m, uint64_t pmask, uint32_t* err,
                           int grid, hipStream_t s) {
   if (m <= 0) return hipSuccess;
   const int64_t TT = (m + kSegTile - 1) / kSegTile;
+#ifdef LSB_SEG_GRID_PER_CU  // A/B: workgroups per CU (the runtime passes 3)
+  grid = grid / 3 * LSB_SEG_GRID_PER_CU;
+#endif
   int64_t g = grid < 1 ? 1 : grid;
   if (g > TT) g = TT;
   hipLaunchKernelGGL(k_segsort, dim3((unsigned)g), dim3(kSegBlock), 0, s, in, out, m, pmask, err);

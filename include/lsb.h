@@ -104,13 +104,17 @@ typedef struct lsb_ctx lsb_ctx_t;
                                       and each rank's block in the whole-key form): 0 (default)
                                       the LSD passes; 1 the hybrid: stable 8-bit passes on the k
                                       most significant varying bytes only (k = 4 at 2^30 records),
-                                      then ONE segmented local sort (k_segsort) orders every run
-                                      of records equal on those bytes by the whole key.  Same
-                                      output (the stable sort by key) from k + 1 passes over HBM
-                                      instead of up to 8.  Skewed keys (one bucket of the first
-                                      byte over 1/32 of the records) take the LSD passes; a
-                                      segment longer than 1024 records makes the sort redo the
-                                      kept input by the LSD passes.  Needs a third buffer. */
+                                      the last of which also orders every segment (run of records
+                                      equal on those bytes, ~0.25 records on average) by the whole
+                                      key inside its tile, and k_segfix merges the segments split
+                                      between two tiles; 2 the same passes, then a separate
+                                      segmented sort (k_segsort) orders the segments.  Same output
+                                      (the stable sort by key) from k passes over HBM instead of up
+                                      to 8.  Skewed keys (one bucket of the first byte over 1/32 of
+                                      the records) take the LSD passes; runs too long for k_segfix
+                                      take k_segsort, and segments longer than 1024 records make
+                                      the sort redo the kept input by the LSD passes.  Needs a
+                                      third record buffer. */
 
 /* ---- geometry: DistributedArray::create (mpi/mpi_lsbsort.cpp:144-149) ---- */
 int64_t lsb_per_rank(int64_t n_total, int num_ranks);            /* ceil(n/P) */

@@ -1,6 +1,9 @@
 """Hybrid local sort (LSB_OPT_HYBRID): k stable k_onesweep passes on the
-most significant varying bytes, then k_segsort orders every segment (run of
-records equal on those bytes) by the whole key.
+most significant varying bytes; every segment (run of records equal on
+those bytes) is then ordered by the whole key: by the last pass itself,
+inside each tile, plus k_segfix for the segments split between tiles
+(mode 1, the default), or by a separate k_segsort pass (mode 2, and the
+fallback of mode 1 when a run crossing a tile is too long).
 
 The output must be the reference's: the stable sort by key
 (mpi/mpi_lsbsort.cpp:580-585 produces it by LSD passes; the verify at
@@ -20,9 +23,9 @@ pytestmark = pytest.mark.gpu
 T = 4096
 
 
-def _sort(lsbsort, a, skip=1, split=0, timing=False):
+def _sort(lsbsort, a, skip=1, split=0, timing=False, mode=1):
     with lsbsort.World(a.size, ranks=1) as w:
-        w.set_option(lsbsort.OPT_HYBRID, 1)
+        w.set_option(lsbsort.OPT_HYBRID, mode)
         w.set_option(lsbsort.OPT_SKIP_CONSTANT_DIGITS, skip)
         w.set_option(lsbsort.OPT_ONESWEEP_SPLIT, split)
         w.set_timing(timing)
@@ -42,9 +45,10 @@ def _uniform(n, seed):
 
 @pytest.mark.parametrize("n", [1, 2, 100, 128, 129, 1000, T - 1, T, T + 1, 2 * T + 3, 10_000, 65_537,
                                1 << 20, (1 << 20) + 12_345, 1 << 22])
-def test_sizes_bit_exact(lsb_built, oracle_mod, n):
+@pytest.mark.parametrize("mode", [1, 2])
+def test_sizes_bit_exact(lsb_built, oracle_mod, n, mode):
     a = _uniform(n, n)
-    out, (lp, ex, _), _ = _sort(lsb_built, a)
+    out, (lp, ex, _), _ = _sort(lsb_built, a, mode=mode)
     assert np.array_equal(out, oracle_mod.stable_sort(a))
     # k MSD passes + one segmented sort: fewer passes than the 8 LSD ones
     # (tiny blocks look skewed to the 1/32 rule and take the LSD passes)
@@ -53,25 +57,28 @@ def test_sizes_bit_exact(lsb_built, oracle_mod, n):
 
 @pytest.mark.parametrize("n,k", [(256, 1), (257, 2), (1000, 2), (1 << 16, 2), (1 << 22, 3),
                                  ((1 << 24) + 1, 4)])
-def test_msd_byte_count(lsb_built, oracle_mod, n, k):
+@pytest.mark.parametrize("mode", [1, 2])
+def test_msd_byte_count(lsb_built, oracle_mod, n, k, mode):
     """k = the fewest top bytes whose varying bits reach ceil(log2 n);
     the per-pass stats show the k byte passes (top bytes, least significant
-    first) and the segmented sort (shift 64)."""
+    first) and, in mode 2, the segmented sort (shift 64)."""
     a = _uniform(n, 7 * n)
-    out, (lp, _, _), rows = _sort(lsb_built, a, timing=True)
+    out, (lp, _, _), rows = _sort(lsb_built, a, timing=True, mode=mode)
     assert np.array_equal(out, oracle_mod.stable_sort(a))
-    assert lp == k + 1
-    assert [r["shift"] for r in rows] == [8 * (8 - k + i) for i in range(k)] + [64]
+    seg = [64] if mode == 2 else []
+    assert lp == k + len(seg)
+    assert [r["shift"] for r in rows] == [8 * (8 - k + i) for i in range(k)] + seg
     assert all(r["elems"] == n for r in rows)
 
 
 @pytest.mark.parametrize("name", ["all_equal", "two_keys", "hot_bucket", "high_bits_only",
                                   "zipf", "sorted", "reverse", "small_range"])
 @pytest.mark.parametrize("n", [200_003, 1 << 21])
-def test_distributions_bit_exact(lsb_built, oracle_mod, name, n):
+@pytest.mark.parametrize("mode", [1, 2])
+def test_distributions_bit_exact(lsb_built, oracle_mod, name, n, mode):
     rng = np.random.default_rng(hash((name, n)) & 0xFFFF)
     a = _dist(name, n, rng)
-    out, _, _ = _sort(lsb_built, a)
+    out, _, _ = _sort(lsb_built, a, mode=mode)
     assert np.array_equal(out, oracle_mod.stable_sort(a))
 
 
@@ -86,19 +93,38 @@ def test_skip_constant_digits_off(lsb_built, oracle_mod):
     a = _uniform(500_009, 3)
     out, (lp, _, _), _ = _sort(lsb_built, a, skip=0)
     assert np.array_equal(out, oracle_mod.stable_sort(a))
-    assert lp == 4  # 3 top bytes (guessed from n alone) + the segmented sort
+    assert lp == 3  # 3 top bytes (guessed from n alone); the last one orders the segments
 
 
-def test_duplicate_keys_keep_input_order(lsb_built, oracle_mod):
-    """Equal keys share a segment; k_segsort ranks them by input position."""
+@pytest.mark.parametrize("mode", [1, 2])
+def test_duplicate_keys_keep_input_order(lsb_built, oracle_mod, mode):
+    """Equal keys share a segment, also across tiles (k_segfix keeps tile
+    t's records first); they are ranked by input position."""
     rng = np.random.default_rng(11)
     n = 1 << 20
     a = np.zeros(n, dtype=DT)
     pool = rng.integers(0, 2**64 - 1, n // 8, dtype=np.uint64)
     a["key"] = pool[rng.integers(0, pool.size, n)]
     a["val"] = np.arange(n, dtype=np.uint64)
-    out, _, _ = _sort(lsb_built, a)
+    out, _, _ = _sort(lsb_built, a, mode=mode)
     assert np.array_equal(out, oracle_mod.stable_sort(a))
+
+
+def test_long_runs_take_the_segment_sort(lsb_built, oracle_mod):
+    """Runs of records equal on all but the last pass's byte hold ~2048
+    records, past the kSegCap slots a tile reports for k_segfix: the fused
+    pass flags it and a k_segsort pass orders the (small) segments."""
+    rng = np.random.default_rng(5)
+    n = 1 << 22
+    mid = rng.integers(0, 1 << 16, 2048, dtype=np.uint64)  # bytes 5-6: 2048 values
+    a = np.zeros(n, dtype=DT)
+    a["key"] = ((rng.integers(0, 256, n, dtype=np.uint64) << np.uint64(56)) |
+                (mid[rng.integers(0, mid.size, n)] << np.uint64(40)) |
+                rng.integers(0, 1 << 40, n, dtype=np.uint64))
+    a["val"] = np.arange(n, dtype=np.uint64)
+    out, (lp, _, _), _ = _sort(lsb_built, a)
+    assert np.array_equal(out, oracle_mod.stable_sort(a))
+    assert lp == 3 + 1  # 3 byte passes + the segmented sort
 
 
 @pytest.mark.parametrize("bases", [1024, 4096])
@@ -114,7 +140,7 @@ def test_long_segments_fall_back_to_lsd(lsb_built, oracle_mod, bases):
     a["val"] = np.arange(n, dtype=np.uint64)
     out, (lp, _, _), _ = _sort(lsb_built, a)
     assert np.array_equal(out, oracle_mod.stable_sort(a))
-    assert lp == 3 + 1 + 8  # 3 byte passes + the failed segmented sort + the LSD passes
+    assert lp == 3 + 1 + 8  # 3 byte passes + the failed segment sorts + the LSD passes
 
 
 def test_generated_input_verifies(lsb_built, digests, oracle_mod):
@@ -134,8 +160,8 @@ def test_repeated_sorts_on_one_context(lsb_built, oracle_mod):
     shared with the LSD passes of the same context."""
     n = 300_007
     with lsb_built.World(n, ranks=1) as w:
-        for i in range(4):
-            w.set_option(lsb_built.OPT_HYBRID, i % 2)
+        for i in range(6):
+            w.set_option(lsb_built.OPT_HYBRID, i % 3)
             a = _uniform(n, 100 + i)
             w.copy_in(0, a)
             w.my_sort()
@@ -158,4 +184,4 @@ def test_whole_key_local_sorts(lsb_built, oracle_mod, digests, P):
 def test_option_range(lsb_built):
     with lsb_built.World(10, ranks=1) as w:
         with pytest.raises(lsb_built.LsbError):
-            w.set_option(lsb_built.OPT_HYBRID, 2)
+            w.set_option(lsb_built.OPT_HYBRID, 3)

@@ -23,7 +23,7 @@ if os.environ.get("LSB_FORCE_EXCHANGE") == "1":
 # LSB_PASSES=reduce-scan: count + scan + scatter per pass instead of single-read passes
 w.set_option(lsbsort.OPT_ONESWEEP, 0 if os.environ.get("LSB_PASSES") == "reduce-scan" else 1)
 # LSB_PASSES=hybrid: k top-byte passes + the segmented local sort (LSB_OPT_HYBRID)
-w.set_option(lsbsort.OPT_HYBRID, 1 if os.environ.get("LSB_PASSES") == "hybrid" else 0)
+w.set_option(lsbsort.OPT_HYBRID, {"hybrid": 1, "hybrid-segsort": 2}.get(os.environ.get("LSB_PASSES", ""), 0))
 w.set_timing(True)
 names = ["upsweep", "scan", "scatter", "exchange", "place", "segsort", "sort"]
 for rep in range(2):
