@@ -126,17 +126,22 @@ hipError_t onesweep_profile(unsigned long long* out10, bool reset);
 // needed.  A segment lies inside one run of records equal on rmask (pmask
 // without this pass's byte), and the pass's input is sorted by rmask; only
 // runs that cross a tile boundary can leave a segment split between two
-// tiles.  For those the pass records the output slot of every record of its
-// first and last run (pos[tile][0][i]: record i of the last run, pos[tile]
-// [1][i]: record i of the first run, input order; meta[tile][0..1] = their
-// counts, 0 when the run does not cross), and launch_segfix merges the
-// split segments.  *err |= 1 when a run holds more than kSegCap records or a
-// segment more than kSegMax (the runtime then runs k_segsort on the output).
-constexpr int kSegCap = 512;
+// tiles.  For those the pass lists every record of its last and first run
+// with its output slot (list[tile][0][*]: the last run, when it crosses
+// into the next tile; list[tile][1][*]: the first run, when it crossed from
+// the previous one; any order; meta[tile][0..1] = their lengths), and
+// launch_segfix merges the split segments.  *err |= 1 when a run holds more
+// than kSegCap records or a segment more than kSegMax (the runtime then runs
+// k_segsort on the output).
+constexpr int kSegCap = 256;
+struct SegEntry {
+  int64_t slot;
+  uint64_t key, val;
+};
 struct SegPass {
   uint64_t pmask = 0;
   uint64_t rmask = 0;
-  int64_t* pos = nullptr;
+  SegEntry* list = nullptr;
   uint32_t* meta = nullptr;
   uint32_t* err = nullptr;
 };
@@ -166,7 +171,7 @@ hipError_t launch_segsort(const Elem* in, Elem* out, int64_t m, uint64_t pmask, 
                           int grid, hipStream_t s);
 // After a SegPass launch over m records on the byte at `shift`: merge every
 // segment split between tiles t and t + 1 (both tiles' crossing runs, from
-// seg.pos / seg.meta), in place in `out`.
+// seg.list / seg.meta), in place in `out`.
 hipError_t launch_segfix(Elem* out, int64_t m, int shift, const SegPass& seg, int grid, hipStream_t s);
 
 // Receiver-side placement of one source's received range: src[i] (receive

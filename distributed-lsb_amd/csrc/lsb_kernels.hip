@@ -765,10 +765,12 @@ __device__ unsigned long long g_os_prof[10];
 // orders each segment (records equal on seg.pmask; inside the tile they are
 // adjacent in the stage, in one bucket run) by the whole key: a record's slot
 // in its run is its segment's first slot + #(segment keys < mine) + #(equal
-// keys staged before me), found by walking its stage neighbours (segments
-// hold ~0.25 records on average at the runtime's choice of bytes).  The
-// records of the tile's first and last rmask runs, when those cross the tile
-// boundary, report their output slots for launch_segfix.
+// keys staged before me).  Segments hold ~0.25 records on average at the
+// runtime's choice of bytes, so a record first compares its two stage
+// neighbours, which are its neighbouring lanes (DPP), and walks the stage in
+// LDS only when one of them shares its segment.  The records of the tile's
+// first and last rmask runs, when those cross the tile boundary, append
+// themselves with their output slot to the tile's lists for launch_segfix.
 template <int BLOCK, int IPT, bool NEXT, bool C16, int HALVES, bool SEG = false>
 __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_onesweep(
     const Elem* __restrict__ in, Elem* __restrict__ out, int64_t m, int shift, int next_shift,
@@ -796,8 +798,7 @@ __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_
   __shared__ uint32_t scan32[W];
   __shared__ int32_t s_tile, s_sub;
   __shared__ uint32_t tile_lo[2];  // C16: low byte of the tile's first, last record
-  __shared__ uint16_t org[SEG ? HT : 1];  // SEG: tile-local input index of each staged record
-  __shared__ int32_t s_rl, s_rf;          // SEG: first index of the last run, end of the first
+  __shared__ uint32_t s_nl, s_nr;  // SEG: records listed of the last run, of the first run
 
   const int t = threadIdx.x;
   const bool bkt = BLOCK == kBuckets || t < kBuckets;  // a bucket thread
@@ -876,8 +877,8 @@ __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_
       s_tile = nxt_tile;
       s_sub = nxt_sub;
       if (SEG) {
-        s_rl = T;
-        s_rf = 0;
+        s_nl = 0;
+        s_nr = 0;
       }
     }
 #pragma unroll
@@ -956,12 +957,6 @@ __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_
       const uint32_t pre = wcnt[w][d];
       rk[i] = pre + below;
       if (valid && below == 0) wcnt[w][d] = (WC)(pre + (uint32_t)__popcll(mt));
-      if (SEG && valid) {
-        const uint64_t rk_ = e[i].key & seg.rmask;
-        const int li = wbase + i * 64;
-        if (cross_l && rk_ == run_l) atomicMin(&s_rl, li);
-        if (cross_f && rk_ == run_f) atomicMax(&s_rf, li + 1);
-      }
       if (C16) {
         const int li = wbase + i * 64;
         if (li == 0) tile_lo[0] = (uint32_t)(e[i].key >> shift16) & 0xFFu;
@@ -1015,7 +1010,6 @@ __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_
           const uint32_t d = (uint32_t)(e[i].key >> shift) & (kBuckets - 1);
           if (HALVES == 1) {
             stage[wcnt[w][d] + rk[i]] = e[i];
-            if (SEG) org[wcnt[w][d] + rk[i]] = (uint16_t)(wbase + i * 64);
           } else {
             if (h == 0) rk[i] += wcnt[w][d];
             if ((int)(rk[i] / HT) == h) stage[rk[i] - h * HT] = e[i];
@@ -1091,22 +1085,6 @@ __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_
 #endif
     if (t == 0) grab(nxt_tile, nxt_sub);  // in flight during the writes
 
-    // SEG: the crossing runs' records report their slots (none past kSegCap:
-    // *seg.err, and k_segsort orders the output instead).
-    int rl = nvalid, rf = 0;
-    if (SEG) {
-      const int nl = cross_l ? nvalid - s_rl : 0, nr = cross_f ? s_rf : 0;
-      const bool over = nl > kSegCap || nr > kSegCap;
-      if (t == 0) {
-        seg.meta[2 * (int64_t)tile] = over ? 0u : (uint32_t)nl;
-        seg.meta[2 * (int64_t)tile + 1] = over ? 0u : (uint32_t)nr;
-        if (over) atomicOr(seg.err, 1u);
-      }
-      if (!over) {
-        rl = nvalid - nl;
-        rf = nr;
-      }
-    }
     // The loop is instantiated twice (the launch-uniform `skewed` picks one
     // outside it): a per-record branch on it cost uniform keys 2.4 %.
     auto write_out = [&](auto skew_tag, int h) {
@@ -1117,32 +1095,45 @@ __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_
         const uint32_t d = (uint32_t)(v.key >> shift) & (kBuckets - 1);
         int pos = j;
         if (SEG) {
-          // The segment's neighbours in the stage (bounded: kSegMax).
+          // Stage neighbours j - 1 and j + 1 are the neighbouring lanes'
+          // records (the wave's j are consecutive; lanes 0 and 63 read LDS).
+          const uint32_t kl = (uint32_t)v.key, kh = (uint32_t)(v.key >> 32);
+          uint64_t pv = ((uint64_t)(uint32_t)__builtin_amdgcn_update_dpp(0, (int)kh, 0x138, 0xf, 0xf, false) << 32) |
+                        (uint32_t)__builtin_amdgcn_update_dpp(0, (int)kl, 0x138, 0xf, 0xf, false);
+          uint64_t nx = ((uint64_t)(uint32_t)__builtin_amdgcn_update_dpp(0, (int)kh, 0x130, 0xf, 0xf, false) << 32) |
+                        (uint32_t)__builtin_amdgcn_update_dpp(0, (int)kl, 0x130, 0xf, 0xf, false);
+          if (lane == 0 && j > 0) pv = stage[j - 1].key;
+          if ((lane == 63 || j + 1 == jend) && j + 1 < nvalid) nx = stage[j + 1].key;
           const uint64_t pk = v.key & seg.pmask;
-          uint32_t less = 0, eqb = 0;
-          int k = j - 1;
-          const int klo = j - kSegMax > 0 ? j - kSegMax : 0;
-          while (k >= klo) {
-            const uint64_t kk = stage[k].key;
-            if ((kk & seg.pmask) != pk) break;
-            less += kk < v.key ? 1u : 0u;
-            eqb += kk == v.key ? 1u : 0u;
-            --k;
+          const bool sp = j > 0 && (pv & seg.pmask) == pk;
+          const bool sn = j + 1 < nvalid && (nx & seg.pmask) == pk;
+          if (sp || sn) {
+            // Walk the segment in LDS (bounded: kSegMax each way).
+            uint32_t less = 0, eqb = 0;
+            int k = j - 1;
+            const int klo = j - kSegMax > 0 ? j - kSegMax : 0;
+            while (k >= klo) {
+              const uint64_t kk = stage[k].key;
+              if ((kk & seg.pmask) != pk) break;
+              less += kk < v.key ? 1u : 0u;
+              eqb += kk == v.key ? 1u : 0u;
+              --k;
+            }
+            const int sfirst = k + 1;  // the segment's first stage slot
+            // kSegMax records walked without leaving the segment: too long
+            bool too_long = k < klo && klo > 0;
+            const int khi = j + 1 + kSegMax < nvalid ? j + 1 + kSegMax : nvalid;
+            k = j + 1;
+            while (k < khi) {
+              const uint64_t kk = stage[k].key;
+              if ((kk & seg.pmask) != pk) break;
+              less += kk < v.key ? 1u : 0u;
+              ++k;
+            }
+            too_long |= k == khi && khi < nvalid;
+            if (too_long) atomicOr(seg.err, 1u);
+            pos = sfirst + (int)(less + eqb);
           }
-          const int first = k + 1;
-          // kSegMax records walked without leaving the segment: too long
-          bool too_long = k < klo && klo > 0;
-          const int khi = j + 1 + kSegMax < nvalid ? j + 1 + kSegMax : nvalid;
-          k = j + 1;
-          while (k < khi) {
-            const uint64_t kk = stage[k].key;
-            if ((kk & seg.pmask) != pk) break;
-            less += kk < v.key ? 1u : 0u;
-            ++k;
-          }
-          too_long |= k == khi && khi < nvalid;
-          if (too_long) atomicOr(seg.err, 1u);
-          pos = first + (int)(less + eqb);
         }
         const int64_t g = delta[d] + pos;
         LSB_DASSERT(g >= 0 && g < m);
@@ -1152,9 +1143,16 @@ __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_
         const uint64_t gs = (uint64_t)g < (uint64_t)(m - 1) ? (uint64_t)g : (uint64_t)(m - 1);
         store_elem(out + gs, v);
         if (SEG) {
-          const int li = org[j];
-          if (li >= rl) seg.pos[(2 * (int64_t)tile) * kSegCap + (li - rl)] = (int64_t)gs;
-          if (li < rf) seg.pos[(2 * (int64_t)tile + 1) * kSegCap + li] = (int64_t)gs;
+          // A record of a crossing run lists itself (slot, key, val).
+          const uint64_t rk_ = v.key & seg.rmask;
+          if (cross_l && rk_ == run_l) {
+            const uint32_t q = atomicAdd(&s_nl, 1u);
+            if (q < (uint32_t)kSegCap) seg.list[(2 * (int64_t)tile) * kSegCap + q] = SegEntry{(int64_t)gs, v.key, v.val};
+          }
+          if (cross_f && rk_ == run_f) {
+            const uint32_t q = atomicAdd(&s_nr, 1u);
+            if (q < (uint32_t)kSegCap) seg.list[(2 * (int64_t)tile + 1) * kSegCap + q] = SegEntry{(int64_t)gs, v.key, v.val};
+          }
         }
         if (NEXT) {
           const uint32_t c = cut[d];
@@ -1207,6 +1205,12 @@ __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_
         }
       }
       __syncthreads();
+    }
+    if (SEG && t == 0) {  // the lists' lengths, none past kSegCap (then k_segsort orders the output)
+      const bool over = s_nl > (uint32_t)kSegCap || s_nr > (uint32_t)kSegCap;
+      seg.meta[2 * (int64_t)tile] = over ? 0u : s_nl;
+      seg.meta[2 * (int64_t)tile + 1] = over ? 0u : s_nr;
+      if (over) atomicOr(seg.err, 1u);
     }
     OS_MARK(4);  // write
   }
@@ -1768,7 +1772,7 @@ hipError_t launch_onesweep(const Elem* in, Elem* out, int64_t m, int shift, int 
   uint32_t* st = status;
   if (extra.seg) {
     // The hybrid's last pass: no next digit, no 16-bit counts, whole stage.
-    if (next_shift >= 0 || c16 || extra.halves != 1 || !extra.seg->pos || !extra.seg->meta ||
+    if (next_shift >= 0 || c16 || extra.halves != 1 || !extra.seg->list || !extra.seg->meta ||
         !extra.seg->err)
       return hipErrorInvalidValue;
     hipLaunchKernelGGL((k_onesweep<kOsBlock, kOsIpt, false, false, 1, true>), gd, bd, 0, s, in, out, m,

@@ -97,7 +97,7 @@ struct Rank {
   int os_halves = 1;                    // this sort's k_onesweep stage split (1 or 2)
   uint32_t os_epoch = 0;                // last look-back epoch
   bool os_dirty = false;                // a launch failed: zero os_status before the next
-  int64_t* seg_pos = nullptr;           // [tiles][2][kSegCap] the hybrid's crossing-run slots
+  lsb::SegEntry* seg_list = nullptr;    // [tiles][2][kSegCap] the hybrid's crossing-run records
   uint32_t* seg_meta = nullptr;         // [tiles][2] their counts
   int os_grid = 0;                      // persistent grid (2 workgroups per CU)
   // Per-digit exchange with single-read local passes (sort_exchange_onesweep):
@@ -366,7 +366,7 @@ void free_rank(Rank& r) {
   (void)hipHostFree(r.split_h);
   (void)hipFree(r.merge_path);
   (void)hipFree(r.os_status);
-  (void)hipFree(r.seg_pos);
+  (void)hipFree(r.seg_list);
   (void)hipFree(r.seg_meta);
   (void)hipFree(r.os_hist);
   (void)hipFree(r.os_ctr);
@@ -1148,11 +1148,11 @@ int sort_hybrid_rank(lsb_ctx* c, Rank& r, int* passes, uint64_t* varying) {
     lsb::SegPass sp;
     if (fuse) {
       const size_t tiles = (size_t)lsb::onesweep_tiles(m);
-      if (!r.seg_pos) LSB_TRY(dev_alloc(&r.seg_pos, tiles * 2 * lsb::kSegCap));
+      if (!r.seg_list) LSB_TRY(dev_alloc(&r.seg_list, tiles * 2 * lsb::kSegCap));
       if (!r.seg_meta) LSB_TRY(dev_alloc(&r.seg_meta, tiles * 2));
       sp.pmask = pmask;
       sp.rmask = pmask & ~((uint64_t)(lsb::kBuckets - 1) << (msd.back() * lsb::kDigitBits));
-      sp.pos = r.seg_pos;
+      sp.list = r.seg_list;
       sp.meta = r.seg_meta;
       sp.err = err;
     }
@@ -1180,7 +1180,8 @@ int sort_hybrid_rank(lsb_ctx* c, Rank& r, int* passes, uint64_t* varying) {
     if (fuse) {
       {
         Timer t(c, &r, LSB_K_SEGSORT);
-        HIP_TRY(lsb::launch_segfix(r.A, m, msd.back() * lsb::kDigitBits, sp, 2 * r.os_grid, r.stream));
+        // one wave per tile boundary, 32 waves per CU
+        HIP_TRY(lsb::launch_segfix(r.A, m, msd.back() * lsb::kDigitBits, sp, 16 * r.os_grid, r.stream));
       }
       uint32_t e = 0;
       LSB_TRY(sync_err(&e));

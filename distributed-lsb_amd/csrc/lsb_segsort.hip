@@ -201,79 +201,66 @@ __global__ __launch_bounds__(kSegBlock) __attribute__((amdgpu_waves_per_eu(LSB_S
 // one rmask run, and only the run crossing the boundary between tiles t and
 // t + 1 has records on both sides.  Each side sorted its part in the stage
 // (k_onesweep SEG), and both parts sit in adjacent slots: the end of tile
-// t's bucket run, then the start of tile t + 1's.  One workgroup per
-// boundary gathers both crossing runs (slots from seg.pos), and for every
-// bucket present on both sides merges the two sorted parts, stably (tile t's
-// records first on equal keys), back into the same slots.
-constexpr int kFixBlock = 256;
+// t's bucket run, then the start of tile t + 1's.  One wave per boundary
+// reads both tiles' lists of the crossing run (slot, key, val), and for
+// every bucket present on both sides merges the two sorted parts, stably
+// (tile t's records first on equal keys), back into the same slots.  A
+// record's new slot: its bucket's first slot on tile t's side + its rank on
+// its own side (slot order, which is key order) + the other side's records
+// before it.  ~64 records per boundary: loops over LDS broadcasts.
+constexpr int kFixWaves = 4;  // boundaries per workgroup (one per wave)
+constexpr int kFixLds = 128;  // list entries a wave stages in LDS (more: read from L2)
 
-__global__ __launch_bounds__(kFixBlock) void k_segfix(Elem* __restrict__ out, int64_t m, int shift,
-                                                      int64_t TT, SegPass seg) {
-  __shared__ uint64_t lk[kSegCap], lv[kSegCap], rk[kSegCap], rv[kSegCap];
-  __shared__ int64_t lp[kSegCap], rp[kSegCap];
-  const int t = threadIdx.x;
-  for (int64_t b = blockIdx.x; b + 1 < TT; b += gridDim.x) {
+__global__ __launch_bounds__(64 * kFixWaves) void k_segfix(Elem* __restrict__ out, int64_t m, int shift,
+                                                           int64_t TT, SegPass seg) {
+  __shared__ SegEntry buf[kFixWaves][kFixLds];  // left part, then right part
+  const int w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  SegEntry* e = buf[w];
+  for (int64_t b = (int64_t)blockIdx.x * kFixWaves + w; b + 1 < TT; b += (int64_t)gridDim.x * kFixWaves) {
     const int nl = (int)seg.meta[2 * b];
     const int nr = (int)seg.meta[2 * (b + 1) + 1];
-    if (nl == 0 || nr == 0) continue;  // the same for the whole workgroup
-    const int64_t* pl = seg.pos + (2 * b) * kSegCap;
-    const int64_t* pr = seg.pos + (2 * (b + 1) + 1) * kSegCap;
-    for (int i = t; i < nl; i += kFixBlock) {
-      int64_t q = pl[i];
-      q = q < 0 ? 0 : (q < m ? q : m - 1);
-      const Elem x = out[q];
-      lp[i] = q;
-      lk[i] = x.key;
-      lv[i] = x.val;
-    }
-    for (int i = t; i < nr; i += kFixBlock) {
-      int64_t q = pr[i];
-      q = q < 0 ? 0 : (q < m ? q : m - 1);
-      const Elem x = out[q];
-      rp[i] = q;
-      rk[i] = x.key;
-      rv[i] = x.val;
-    }
-    __syncthreads();
-    // New slot of each record of a bucket present on both sides: the
-    // bucket's first slot (its first record of tile t) + its rank on its
-    // own side (slot order = key order) + the other side's records before it.
-    constexpr int kPer = (2 * kSegCap + kFixBlock - 1) / kFixBlock;
-    int64_t dst[kPer];
-    int cnt = 0;
-    for (int x = t; x < nl + nr; x += kFixBlock, ++cnt) {
-      dst[cnt] = -1;
-      const bool left = x < nl;
-      const int i = left ? x : x - nl;
-      const uint64_t key = left ? lk[i] : rk[i];
-      const int64_t slot = left ? lp[i] : rp[i];
-      const uint32_t c = (uint32_t)(key >> shift) & (kBuckets - 1);
-      int64_t start = INT64_MAX;
-      int own = 0, other = 0, in_l = 0, in_r = 0;
-      for (int y = 0; y < nl; ++y) {
-        if (((uint32_t)(lk[y] >> shift) & (kBuckets - 1)) != c) continue;
-        ++in_l;
-        start = lp[y] < start ? lp[y] : start;
-        if (left) own += lp[y] < slot ? 1 : 0;
-        else other += lk[y] <= key ? 1 : 0;
+    if (nl == 0 || nr == 0) continue;  // the same for the whole wave
+    const SegEntry* L = seg.list + (2 * b) * kSegCap;
+    const SegEntry* R = seg.list + (2 * (b + 1) + 1) * kSegCap;
+    const int n = nl + nr;
+    auto merge = [&](auto get) {
+      for (int x = lane; x < n; x += 64) {
+        const bool left = x < nl;
+        const SegEntry me = get(x);
+        const uint32_t c = (uint32_t)(me.key >> shift) & (kBuckets - 1);
+        int64_t start = INT64_MAX;
+        int own = 0, other = 0, in_l = 0, in_r = 0;
+        for (int y = 0; y < n; ++y) {
+          const SegEntry o = get(y);
+          if (((uint32_t)(o.key >> shift) & (kBuckets - 1)) != c) continue;
+          if (y < nl) {
+            ++in_l;
+            start = o.slot < start ? o.slot : start;
+            if (left) own += o.slot < me.slot ? 1 : 0;
+            else other += o.key <= me.key ? 1 : 0;
+          } else {
+            ++in_r;
+            if (left) other += o.key < me.key ? 1 : 0;
+            else own += o.slot < me.slot ? 1 : 0;
+          }
+        }
+        if (in_l > 0 && in_r > 0) {
+          const int64_t g = start + own + other;
+          if (g >= 0 && g < m) out[g] = Elem{me.key, me.val};
+        }
       }
-      for (int y = 0; y < nr; ++y) {
-        if (((uint32_t)(rk[y] >> shift) & (kBuckets - 1)) != c) continue;
-        ++in_r;
-        if (left) other += rk[y] < key ? 1 : 0;
-        else own += rp[y] < slot ? 1 : 0;
-      }
-      if (in_l > 0 && in_r > 0) dst[cnt] = start + own + other;
+    };
+    if (n <= kFixLds) {
+      for (int i = lane; i < n; i += 64) e[i] = i < nl ? L[i] : R[i - nl];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      merge([&](int y) { return e[y]; });
+      __builtin_amdgcn_wave_barrier();  // e[] is rewritten for the next boundary
+    } else {  // a long crossing run: the lists straight from L2
+      merge([&](int y) { return y < nl ? L[y] : R[y - nl]; });
     }
-    __syncthreads();  // every record is read before any is rewritten
-    cnt = 0;
-    for (int x = t; x < nl + nr; x += kFixBlock, ++cnt) {
-      if (dst[cnt] < 0 || dst[cnt] >= m) continue;
-      const bool left = x < nl;
-      const int i = left ? x : x - nl;
-      out[dst[cnt]] = left ? Elem{lk[i], lv[i]} : Elem{rk[i], rv[i]};
-    }
-    __syncthreads();  // lk ... rp are rewritten for the next boundary
   }
 }
 
@@ -285,7 +272,8 @@ hipError_t launch_segfix(Elem* out, int64_t m, int shift, const SegPass& seg, in
   if (TT < 2) return hipSuccess;
   int64_t g = grid < 1 ? 1 : grid;
   if (g > TT - 1) g = TT - 1;
-  hipLaunchKernelGGL(k_segfix, dim3((unsigned)g), dim3(kFixBlock), 0, s, out, m, shift, TT, seg);
+  g = (g + kFixWaves - 1) / kFixWaves;
+  hipLaunchKernelGGL(k_segfix, dim3((unsigned)g), dim3(64 * kFixWaves), 0, s, out, m, shift, TT, seg);
   return hipGetLastError();
 }
 
