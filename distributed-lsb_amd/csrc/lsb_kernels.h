@@ -126,23 +126,17 @@ hipError_t onesweep_profile(unsigned long long* out10, bool reset);
 // needed.  A segment lies inside one run of records equal on rmask (pmask
 // without this pass's byte), and the pass's input is sorted by rmask; only
 // runs that cross a tile boundary can leave a segment split between two
-// tiles.  For those the pass lists every record of its last and first run
-// with its output slot (list[tile][0][*]: the last run, when it crosses
-// into the next tile; list[tile][1][*]: the first run, when it crossed from
-// the previous one; any order; meta[tile][0..1] = their lengths), and
-// launch_segfix merges the split segments.  *err |= 1 when a run holds more
-// than kSegCap records or a segment more than kSegMax (the runtime then runs
+// tiles, and launch_segfix merges those from the pass's input, its look-back
+// rows and base (workgroup 0 writes base[x * 256 + b] = the first output slot
+// of bucket b's sub-array x records).  *err |= 1 when a segment inside a
+// tile holds more than kSegMax records, or a crossing run more than kSegCap
+// on one side of its boundary or spans a whole tile (the runtime then runs
 // k_segsort on the output).
 constexpr int kSegCap = 256;
-struct SegEntry {
-  int64_t slot;
-  uint64_t key, val;
-};
 struct SegPass {
   uint64_t pmask = 0;
   uint64_t rmask = 0;
-  SegEntry* list = nullptr;
-  uint32_t* meta = nullptr;
+  int64_t* base = nullptr;  // kOnesweepSubs * 256
   uint32_t* err = nullptr;
 };
 struct OnesweepExtra {
@@ -169,10 +163,11 @@ hipError_t launch_onesweep(const Elem* in, Elem* out, int64_t m, int shift, int 
 constexpr int kSegMax = 1024;
 hipError_t launch_segsort(const Elem* in, Elem* out, int64_t m, uint64_t pmask, uint32_t* err,
                           int grid, hipStream_t s);
-// After a SegPass launch over m records on the byte at `shift`: merge every
-// segment split between tiles t and t + 1 (both tiles' crossing runs, from
-// seg.list / seg.meta), in place in `out`.
-hipError_t launch_segfix(Elem* out, int64_t m, int shift, const SegPass& seg, int grid, hipStream_t s);
+// After a SegPass launch in -> out over m records on the byte at `shift`
+// (status: that launch's look-back rows): merge every segment split between
+// tiles t and t + 1, in place in `out`.
+hipError_t launch_segfix(const Elem* in, Elem* out, int64_t m, int shift, const uint32_t* status,
+                         const SegPass& seg, int grid, hipStream_t s);
 
 // Receiver-side placement of one source's received range: src[i] (receive
 // index k0 + i) goes to out[off_row[digit] + k0 + i], off_row = the source's

@@ -25,7 +25,7 @@
 //   * The ranked tile is staged in LDS (64 KiB) and written back in
 //     tile-sorted order, so each bucket's run leaves the CU as contiguous
 //     16-byte stores from consecutive lanes.
-#include "lsb_kernels.h"
+#include "lsb_device.h"
 #include <type_traits>
 
 // Debug build (make debug, -DLSB_DEBUG): device-side bounds asserts on every
@@ -621,17 +621,7 @@ constexpr int kStPol = 16;
 typedef __attribute__((address_space(1))) uint32_t gu32;
 typedef uint32_t v2u __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ int64_t sub_first_tile(int x, int64_t TT) { return (int64_t)x * TT / kSub; }
-// Sub-array of tile t without a division: the number of x in 1..kSub-1
-// with x * TT <= kSub * t + kSub - 1, i.e. floor(x * TT / kSub) <= t
-// (32-bit exact: TT < 2^22, see kOnesweepMaxElems).
-__device__ __forceinline__ int sub_of_tile(int64_t t, int64_t TT) {
-  const uint32_t num = (uint32_t)kSub * (uint32_t)t + (uint32_t)(kSub - 1), tt = (uint32_t)TT;
-  int x = 0;
-#pragma unroll
-  for (int k = 1; k < kSub; ++k) x += num >= (uint32_t)k * tt ? 1 : 0;
-  return x;
-}
+// sub_first_tile, sub_of_tile: lsb_device.h
 
 // sub_hist[x * 256 + b] += number of records of sub-array x with digit b;
 // SPAN as in k_upsweep.  Workgroup c walks tiles [c*tpw, (c+1)*tpw).
@@ -768,9 +758,11 @@ __device__ unsigned long long g_os_prof[10];
 // keys staged before me).  Segments hold ~0.25 records on average at the
 // runtime's choice of bytes, so a record first compares its two stage
 // neighbours, which are its neighbouring lanes (DPP), and walks the stage in
-// LDS only when one of them shares its segment.  The records of the tile's
-// first and last rmask runs, when those cross the tile boundary, append
-// themselves with their output slot to the tile's lists for launch_segfix.
+// LDS only when one of them shares its segment.  Segments split between
+// tiles are merged afterwards by launch_segfix, from this pass's input and
+// look-back rows and the bucket bases workgroup 0 writes to seg.base: the
+// pass records nothing per tile (crossing-run lists appended here cost it
+// ~1 ms at 2^30, profiles/r03_ab_seg.log).
 template <int BLOCK, int IPT, bool NEXT, bool C16, int HALVES, bool SEG = false>
 __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_onesweep(
     const Elem* __restrict__ in, Elem* __restrict__ out, int64_t m, int shift, int next_shift,
@@ -798,7 +790,6 @@ __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_
   __shared__ uint32_t scan32[W];
   __shared__ int32_t s_tile, s_sub;
   __shared__ uint32_t tile_lo[2];  // C16: low byte of the tile's first, last record
-  __shared__ uint32_t s_nl, s_nr;  // SEG: records listed of the last run, of the first run
 
   const int t = threadIdx.x;
   const bool bkt = BLOCK == kBuckets || t < kBuckets;  // a bucket thread
@@ -806,7 +797,7 @@ __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_
   const uint32_t lane = lane_id();
   const int64_t TT = (m + T - 1) / T;
   // Granule tags (bits 30-31): this launch's parity, and the prefix bit.
-  constexpr uint32_t kValMask = (1u << 30) - 1u, kPreBit = 1u << 30;
+  constexpr uint32_t kValMask = kStatusValMask, kPreBit = 1u << 30;
   const uint32_t tag_agg = (epoch & 1u) << 31, tag_pre = tag_agg | kPreBit;
   const int shift16 = shift - 8;
   uint32_t acc_lo = 0xFFFFFFFFu;  // C16: thread t's running count of digit (t, acc_lo)
@@ -831,6 +822,14 @@ __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_
   uint64_t all;
   const uint64_t bstart = block_exclusive_scan<BLOCK>(tot, scan64, &all);
   if (totals != nullptr && blockIdx.x == 0 && bkt) totals[t] = tot;
+  if (SEG && blockIdx.x == 0 && bkt) {  // k_segfix's bucket bases per sub-array
+    uint64_t pre = bstart;
+#pragma unroll
+    for (int x = 0; x < kSub; ++x) {
+      seg.base[x * kBuckets + t] = (int64_t)pre;
+      pre += col[x];
+    }
+  }
   // Skewed digit (one bucket holds more than 1/32 of the records, e.g. Zipf
   // keys): runs of equal next digits are then long, and 64 lanes adding to
   // one LDS counter serialise.  Such launches add once per run of equal
@@ -876,10 +875,6 @@ __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_
     if (t == 0) {
       s_tile = nxt_tile;
       s_sub = nxt_sub;
-      if (SEG) {
-        s_nl = 0;
-        s_nr = 0;
-      }
     }
 #pragma unroll
     for (int j = 0; j < kBuckets / 64; ++j) wcnt[w][lane + 64 * j] = 0;
@@ -905,16 +900,6 @@ __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_
     for (int i = 0; i < IPT; ++i) {
       const int li = wbase + i * 64;
       e[i] = li < nvalid ? load_elem_nt(in + tb + li) : Elem{0ull, 0ull};
-    }
-    // SEG: the rmask runs at the tile's two ends, and whether they cross.
-    uint64_t run_f = 0, run_l = 0;
-    bool cross_f = false, cross_l = false;
-    if (SEG) {
-      const uint64_t* keys = reinterpret_cast<const uint64_t*>(in);
-      run_f = keys[2 * tb] & seg.rmask;
-      run_l = keys[2 * (tb + nvalid - 1)] & seg.rmask;
-      cross_f = tb > 0 && (keys[2 * (tb - 1)] & seg.rmask) == run_f;
-      cross_l = tb + nvalid < m && (keys[2 * (tb + nvalid)] & seg.rmask) == run_l;
     }
 #ifdef LSB_OS_PROFILE
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1142,18 +1127,6 @@ __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_
         // clamp, not a branch: the conditional store cost 6 % of the sort.
         const uint64_t gs = (uint64_t)g < (uint64_t)(m - 1) ? (uint64_t)g : (uint64_t)(m - 1);
         store_elem(out + gs, v);
-        if (SEG) {
-          // A record of a crossing run lists itself (slot, key, val).
-          const uint64_t rk_ = v.key & seg.rmask;
-          if (cross_l && rk_ == run_l) {
-            const uint32_t q = atomicAdd(&s_nl, 1u);
-            if (q < (uint32_t)kSegCap) seg.list[(2 * (int64_t)tile) * kSegCap + q] = SegEntry{(int64_t)gs, v.key, v.val};
-          }
-          if (cross_f && rk_ == run_f) {
-            const uint32_t q = atomicAdd(&s_nr, 1u);
-            if (q < (uint32_t)kSegCap) seg.list[(2 * (int64_t)tile + 1) * kSegCap + q] = SegEntry{(int64_t)gs, v.key, v.val};
-          }
-        }
         if (NEXT) {
           const uint32_t c = cut[d];
           const uint32_t xs = (uint32_t)j >= (c & 0xFFFFu) ? (c >> 24) : ((c >> 16) & 0xFFu);
@@ -1205,12 +1178,6 @@ __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_
         }
       }
       __syncthreads();
-    }
-    if (SEG && t == 0) {  // the lists' lengths, none past kSegCap (then k_segsort orders the output)
-      const bool over = s_nl > (uint32_t)kSegCap || s_nr > (uint32_t)kSegCap;
-      seg.meta[2 * (int64_t)tile] = over ? 0u : s_nl;
-      seg.meta[2 * (int64_t)tile + 1] = over ? 0u : s_nr;
-      if (over) atomicOr(seg.err, 1u);
     }
     OS_MARK(4);  // write
   }
@@ -1772,7 +1739,7 @@ hipError_t launch_onesweep(const Elem* in, Elem* out, int64_t m, int shift, int 
   uint32_t* st = status;
   if (extra.seg) {
     // The hybrid's last pass: no next digit, no 16-bit counts, whole stage.
-    if (next_shift >= 0 || c16 || extra.halves != 1 || !extra.seg->list || !extra.seg->meta ||
+    if (next_shift >= 0 || c16 || extra.halves != 1 || !extra.seg->base ||
         !extra.seg->err)
       return hipErrorInvalidValue;
     hipLaunchKernelGGL((k_onesweep<kOsBlock, kOsIpt, false, false, 1, true>), gd, bd, 0, s, in, out, m,

@@ -97,8 +97,7 @@ struct Rank {
   int os_halves = 1;                    // this sort's k_onesweep stage split (1 or 2)
   uint32_t os_epoch = 0;                // last look-back epoch
   bool os_dirty = false;                // a launch failed: zero os_status before the next
-  lsb::SegEntry* seg_list = nullptr;    // [tiles][2][kSegCap] the hybrid's crossing-run records
-  uint32_t* seg_meta = nullptr;         // [tiles][2] their counts
+  int64_t* seg_base = nullptr;          // [kOnesweepSubs][256] the hybrid's bucket bases (k_segfix)
   int os_grid = 0;                      // persistent grid (2 workgroups per CU)
   // Per-digit exchange with single-read local passes (sort_exchange_onesweep):
   // os_hist[os_cur] is A's sub-array histogram of the byte at os_valid (-1:
@@ -366,8 +365,7 @@ void free_rank(Rank& r) {
   (void)hipHostFree(r.split_h);
   (void)hipFree(r.merge_path);
   (void)hipFree(r.os_status);
-  (void)hipFree(r.seg_list);
-  (void)hipFree(r.seg_meta);
+  (void)hipFree(r.seg_base);
   (void)hipFree(r.os_hist);
   (void)hipFree(r.os_ctr);
   (void)hipHostFree(r.os_err_h);
@@ -1147,24 +1145,25 @@ int sort_hybrid_rank(lsb_ctx* c, Rank& r, int* passes, uint64_t* varying) {
     const bool fuse = c->hybrid == 1 && r.os_halves == 1 && !msd.empty();
     lsb::SegPass sp;
     if (fuse) {
-      const size_t tiles = (size_t)lsb::onesweep_tiles(m);
-      if (!r.seg_list) LSB_TRY(dev_alloc(&r.seg_list, tiles * 2 * lsb::kSegCap));
-      if (!r.seg_meta) LSB_TRY(dev_alloc(&r.seg_meta, tiles * 2));
+      if (!r.seg_base) LSB_TRY(dev_alloc(&r.seg_base, (size_t)lsb::kOnesweepSubs * lsb::kBuckets));
       sp.pmask = pmask;
       sp.rmask = pmask & ~((uint64_t)(lsb::kBuckets - 1) << (msd.back() * lsb::kDigitBits));
-      sp.list = r.seg_list;
-      sp.meta = r.seg_meta;
+      sp.base = r.seg_base;
       sp.err = err;
     }
     HIP_TRY(hipMemsetAsync(err, 0, sizeof(uint32_t), r.stream));
     uint32_t* hist[2] = {r.os_hist, r.os_hist + lsb::kOnesweepSubs * lsb::kBuckets};
+    const Elem* seg_in = nullptr;  // the last pass's input, read by k_segfix
     for (size_t i = 0; i < msd.size(); ++i) {
       const int shift = msd[i] * lsb::kDigitBits;
       const int next = i + 1 < msd.size() ? msd[i + 1] * lsb::kDigitBits : -1;
       begin_pass(c, shift);
       lsb::OnesweepExtra x;
       x.halves = r.os_halves;
-      if (fuse && i + 1 == msd.size()) x.seg = &sp;
+      if (fuse && i + 1 == msd.size()) {
+        x.seg = &sp;
+        seg_in = r.A;
+      }
       LSB_TRY(onesweep_launch(c, r, shift, next, hist[i & 1], hist[(i + 1) & 1], x));
       ++*passes;
       if (i == 0) r.B = X2;  // A is X1 now
@@ -1181,7 +1180,8 @@ int sort_hybrid_rank(lsb_ctx* c, Rank& r, int* passes, uint64_t* varying) {
       {
         Timer t(c, &r, LSB_K_SEGSORT);
         // one wave per tile boundary, 32 waves per CU
-        HIP_TRY(lsb::launch_segfix(r.A, m, msd.back() * lsb::kDigitBits, sp, 16 * r.os_grid, r.stream));
+        HIP_TRY(lsb::launch_segfix(seg_in, r.A, m, msd.back() * lsb::kDigitBits, r.os_status, sp,
+                                   16 * r.os_grid, r.stream));
       }
       uint32_t e = 0;
       LSB_TRY(sync_err(&e));

@@ -29,7 +29,7 @@
 // LSD passes (it kept the input).  Records go straight from registers to
 // their slot: a wave's 64 records lie in one or two segments, so its stores
 // permute within a few contiguous lines, which the memory pipeline merges.
-#include "lsb_kernels.h"
+#include "lsb_device.h"
 
 namespace lsb {
 namespace {
@@ -201,79 +201,124 @@ __global__ __launch_bounds__(kSegBlock) __attribute__((amdgpu_waves_per_eu(LSB_S
 // one rmask run, and only the run crossing the boundary between tiles t and
 // t + 1 has records on both sides.  Each side sorted its part in the stage
 // (k_onesweep SEG), and both parts sit in adjacent slots: the end of tile
-// t's bucket run, then the start of tile t + 1's.  One wave per boundary
-// reads both tiles' lists of the crossing run (slot, key, val), and for
-// every bucket present on both sides merges the two sorted parts, stably
-// (tile t's records first on equal keys), back into the same slots.  A
-// record's new slot: its bucket's first slot on tile t's side + its rank on
-// its own side (slot order, which is key order) + the other side's records
-// before it.  ~64 records per boundary: loops over LDS broadcasts.
+// t's bucket-d block, then the start of tile t + 1's, both at
+// P = base[sub-array of t][d] + tile t's inclusive look-back value for d.
+// The pass itself records nothing: one wave per boundary finds the crossing
+// run in the pass's input (records [b - a, b + c) around the boundary b,
+// the pass's input being sorted by rmask), counts both sides per bucket in
+// LDS, and re-places only the records of buckets present on both sides:
+// slot = P - (left count) + #(keys < mine) + #(equal keys before me in the
+// input), over the few such records (~4 buckets of ~64 run records at
+// 2^30).  A run longer than kSegCap on one side, or one spanning a whole
+// tile (its segments then touch three tiles), sets *err: the runtime sorts
+// the segments with k_segsort instead.
 constexpr int kFixWaves = 4;  // boundaries per workgroup (one per wave)
-constexpr int kFixLds = 128;  // list entries a wave stages in LDS (more: read from L2)
 
-__global__ __launch_bounds__(64 * kFixWaves) void k_segfix(Elem* __restrict__ out, int64_t m, int shift,
-                                                           int64_t TT, SegPass seg) {
-  __shared__ SegEntry buf[kFixWaves][kFixLds];  // left part, then right part
+__global__ __launch_bounds__(64 * kFixWaves) void k_segfix(const Elem* __restrict__ in, Elem* __restrict__ out,
+                                                           int64_t m, int shift, int64_t TT,
+                                                           const uint32_t* __restrict__ status, SegPass seg) {
+  __shared__ uint32_t cnt[kFixWaves][kBuckets];     // left count | right count << 16
+  __shared__ uint64_t mkey[kFixWaves][2 * kSegCap];  // the records to re-place: key,
+  __shared__ uint32_t mpos[kFixWaves][2 * kSegCap];  // and position in the run
   const int w = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
-  SegEntry* e = buf[w];
-  for (int64_t b = (int64_t)blockIdx.x * kFixWaves + w; b + 1 < TT; b += (int64_t)gridDim.x * kFixWaves) {
-    const int nl = (int)seg.meta[2 * b];
-    const int nr = (int)seg.meta[2 * (b + 1) + 1];
-    if (nl == 0 || nr == 0) continue;  // the same for the whole wave
-    const SegEntry* L = seg.list + (2 * b) * kSegCap;
-    const SegEntry* R = seg.list + (2 * (b + 1) + 1) * kSegCap;
-    const int n = nl + nr;
-    auto merge = [&](auto get) {
-      for (int x = lane; x < n; x += 64) {
-        const bool left = x < nl;
-        const SegEntry me = get(x);
-        const uint32_t c = (uint32_t)(me.key >> shift) & (kBuckets - 1);
-        int64_t start = INT64_MAX;
-        int own = 0, other = 0, in_l = 0, in_r = 0;
-        for (int y = 0; y < n; ++y) {
-          const SegEntry o = get(y);
-          if (((uint32_t)(o.key >> shift) & (kBuckets - 1)) != c) continue;
-          if (y < nl) {
-            ++in_l;
-            start = o.slot < start ? o.slot : start;
-            if (left) own += o.slot < me.slot ? 1 : 0;
-            else other += o.key <= me.key ? 1 : 0;
-          } else {
-            ++in_r;
-            if (left) other += o.key < me.key ? 1 : 0;
-            else own += o.slot < me.slot ? 1 : 0;
-          }
-        }
-        if (in_l > 0 && in_r > 0) {
-          const int64_t g = start + own + other;
-          if (g >= 0 && g < m) out[g] = Elem{me.key, me.val};
-        }
+  const uint64_t* __restrict__ K = reinterpret_cast<const uint64_t*>(in);
+  auto wave_sync = []() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  };
+  bool bad = false;
+  for (int64_t t = (int64_t)blockIdx.x * kFixWaves + w; t + 1 < TT; t += (int64_t)gridDim.x * kFixWaves) {
+    const int64_t b = (t + 1) * kTile;  // tile t + 1's first record
+    const uint64_t v = K[2 * (b - 1)] & seg.rmask;
+    if ((K[2 * b] & seg.rmask) != v) continue;  // the same for the whole wave
+    const int64_t lo = t * kTile, hi = b + kTile < m ? b + kTile : m;
+    int a = 0, c = 0;  // the run's records before / from b, up to the two tiles' ends
+    for (;;) {
+      const int64_t i = b - 1 - a - lane;
+      const uint64_t stop = __ballot(!(i >= lo && (K[2 * i] & seg.rmask) == v));
+      if (stop) {
+        a += __builtin_ctzll(stop);
+        break;
       }
-    };
-    if (n <= kFixLds) {
-      for (int i = lane; i < n; i += 64) e[i] = i < nl ? L[i] : R[i - nl];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      merge([&](int y) { return e[y]; });
-      __builtin_amdgcn_wave_barrier();  // e[] is rewritten for the next boundary
-    } else {  // a long crossing run: the lists straight from L2
-      merge([&](int y) { return y < nl ? L[y] : R[y - nl]; });
+      a += 64;
+      if (a > kSegCap) break;
     }
+    for (;;) {
+      const int64_t i = b + c + lane;
+      const uint64_t stop = __ballot(!(i < hi && (K[2 * i] & seg.rmask) == v));
+      if (stop) {
+        c += __builtin_ctzll(stop);
+        break;
+      }
+      c += 64;
+      if (c > kSegCap) break;
+    }
+    if (a > kSegCap || c > kSegCap || (b - a == lo && lo > 0 && (K[2 * (lo - 1)] & seg.rmask) == v) ||
+        (b + c == hi && hi < m && (K[2 * hi] & seg.rmask) == v)) {
+      bad = true;
+      continue;
+    }
+    const int n = a + c;
+    const int64_t r0 = b - a;
+    for (int d = lane; d < kBuckets; d += 64) cnt[w][d] = 0;
+    wave_sync();
+    for (int x = lane; x < n; x += 64) {
+      const uint32_t d = (uint32_t)(K[2 * (r0 + x)] >> shift) & (kBuckets - 1);
+      atomicAdd(&cnt[w][d], x < a ? 1u : 0x10000u);
+    }
+    wave_sync();
+    int nm = 0;  // records whose bucket has both sides: compacted in run order
+    for (int x0 = 0; x0 < n; x0 += 64) {
+      const int x = x0 + lane;
+      uint64_t k = 0;
+      bool mv = false;
+      if (x < n) {
+        k = K[2 * (r0 + x)];
+        const uint32_t cc = cnt[w][(uint32_t)(k >> shift) & (kBuckets - 1)];
+        mv = (cc & 0xFFFFu) != 0 && (cc >> 16) != 0;
+      }
+      const uint64_t mb = __ballot(mv);
+      if (mv) {
+        const int q = nm + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mb, 0u));
+        mkey[w][q] = k;
+        mpos[w][q] = (uint32_t)x;
+      }
+      nm += __popcll(mb);
+    }
+    wave_sync();
+    const int x_t = sub_of_tile(t, TT);
+    for (int y = lane; y < nm; y += 64) {
+      const uint64_t k = mkey[w][y];
+      const uint32_t x = mpos[w][y];
+      const uint32_t d = (uint32_t)(k >> shift) & (kBuckets - 1);
+      uint32_t before = 0;
+      for (int z = 0; z < nm; ++z) {
+        const uint64_t kz = mkey[w][z];
+        if (((uint32_t)(kz >> shift) & (kBuckets - 1)) != d) continue;
+        before += (kz < k || (kz == k && mpos[w][z] < x)) ? 1u : 0u;
+      }
+      const int64_t P = seg.base[x_t * kBuckets + d] + (int64_t)(status[t * kBuckets + d] & kStatusValMask);
+      const int64_t g = P - (int64_t)(cnt[w][d] & 0xFFFFu) + (int64_t)before;
+      if (g >= 0 && g < m) out[g] = Elem{k, in[r0 + x].val};
+    }
+    wave_sync();  // cnt, mkey and mpos are rewritten for the next boundary
   }
+  if (bad) atomicOr(seg.err, 1u);
 }
 
 }  // namespace
 
-hipError_t launch_segfix(Elem* out, int64_t m, int shift, const SegPass& seg, int grid, hipStream_t s) {
+hipError_t launch_segfix(const Elem* in, Elem* out, int64_t m, int shift, const uint32_t* status,
+                         const SegPass& seg, int grid, hipStream_t s) {
   if (m <= 0) return hipSuccess;
   const int64_t TT = (m + kTile - 1) / kTile;
   if (TT < 2) return hipSuccess;
   int64_t g = grid < 1 ? 1 : grid;
   if (g > TT - 1) g = TT - 1;
   g = (g + kFixWaves - 1) / kFixWaves;
-  hipLaunchKernelGGL(k_segfix, dim3((unsigned)g), dim3(64 * kFixWaves), 0, s, out, m, shift, TT, seg);
+  hipLaunchKernelGGL(k_segfix, dim3((unsigned)g), dim3(64 * kFixWaves), 0, s, in, out, m, shift, TT, status, seg);
   return hipGetLastError();
 }
 

@@ -201,7 +201,7 @@ def source_digest() -> str:
     import hashlib
     h = hashlib.sha256()
     for rel in ("csrc/lsb_kernels.hip", "csrc/lsb_merge.hip", "csrc/lsb_segsort.hip", "csrc/lsb_runtime.cpp",
-                "csrc/lsb_kernels.h", "../include/lsb.h"):
+                "csrc/lsb_kernels.h", "csrc/lsb_device.h", "../include/lsb.h"):
         with open(os.path.join(ROOT_DIR, rel), "rb") as f:
             h.update(f.read())
     return h.hexdigest()

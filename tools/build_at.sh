@@ -10,7 +10,7 @@ R=$(cd "$(dirname "$0")/.." && pwd)
 mkdir -p "$out/src/distributed-lsb_amd/csrc" "$out/src/include"
 for f in distributed-lsb_amd/csrc/lsb_kernels.hip distributed-lsb_amd/csrc/lsb_merge.hip \
          distributed-lsb_amd/csrc/lsb_segsort.hip \
-         distributed-lsb_amd/csrc/lsb_runtime.cpp distributed-lsb_amd/csrc/lsb_kernels.h include/lsb.h; do
+         distributed-lsb_amd/csrc/lsb_runtime.cpp distributed-lsb_amd/csrc/lsb_kernels.h distributed-lsb_amd/csrc/lsb_device.h include/lsb.h; do
   git -C "$R" show "$rev:$f" > "$out/src/$f" 2>/dev/null || rm -f "$out/src/$f"  # older revisions lack some
 done
 S=$out/src
