@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Summarise a tools/profile.sh run into profiles/.
 
-Reads gpurun_out/prof/{stats,fetch,write}/ (rocprofv3 CSV) and writes
+Reads gpurun_out/prof/{stats,fetch,write}/ (rocprofv3 CSV; or PROF_DIR) and writes
   profiles/<tag>_kernel_stats.csv   rocprofv3 --stats summary (copied)
   profiles/<tag>_pmc.json           per-kernel avg duration and HBM bytes per launch
 
@@ -21,11 +21,16 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+TEMPLATES = False  # --templates: keep template instances apart
+
+
 def short(name):
     """Kernel base name: template instances (k_onesweep<256, 16, true> and
-    <..., false>) are one kernel, averaged over all their launches."""
+    <..., false>) are one kernel, averaged over all their launches (unless
+    --templates: the hybrid's SEG pass is k_onesweep<..., true>)."""
     name = name.replace("(anonymous namespace)::", "").replace("void ", "")
-    return name.split("(")[0].replace("lsb::", "").split("<")[0]
+    name = name.split("(")[0].replace("lsb::", "")
+    return name if TEMPLATES else name.split("<")[0]
 
 
 def per_kernel(path, counter):
@@ -71,4 +76,12 @@ def main(tag, prof=os.path.join(ROOT, "gpurun_out", "prof"),
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "r01")
+    # pmc_summary.py TAG [PROF_DIR [WORKLOAD]] [--templates]
+    args = [a for a in sys.argv[1:] if a != "--templates"]
+    TEMPLATES = len(args) < len(sys.argv) - 1
+    kw = {}
+    if len(args) > 1:
+        kw["prof"] = args[1]
+    if len(args) > 2:
+        kw["workload"] = args[2]
+    main(args[0] if args else "r01", **kw)
