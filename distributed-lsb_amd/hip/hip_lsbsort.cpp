@@ -25,6 +25,9 @@
 //   --exchange alltoallv|p2p|peer  element exchange (default RCCL AllToAllv in
 //              slices; grouped Send/Recv; direct peer stores, the shmem_putmem form)
 //   --slices S  all-to-all slices whose placement overlaps the next slice
+//   --hybrid 0|1|2  local sort by the hybrid (LSB_OPT_HYBRID: k top-byte passes,
+//              then the segments ordered inside the last pass (1) or by a
+//              k_segsort pass (2)); the same output; 0 (default) = LSD passes
 //   --share-gpus G  with --gpus P: rank r runs on device r % G and is its own
 //              RCCL "host" (NCCL_HOSTID), so RCCL links ranks that share a GPU
 //              by its socket transport -- a rehearsal of the multi-GPU path on
@@ -59,6 +62,7 @@ struct Options {
   double zipf_s = 1.1;
   int exchange_option = -1;  // --exchange: LSB_OPT_EXCHANGE_P2P / _PEER, or -1 (AllToAllv)
   int slices = 0;            // --slices S (0: library default)
+  int hybrid = 0;            // --hybrid 0|1|2 (LSB_OPT_HYBRID)
   int64_t test_corrupt = -1; // --test-corrupt I: overwrite sorted record I (tests the report)
   int share_gpus = 0;        // --share-gpus G: rank r on device r % G, one RCCL host per rank
 };
@@ -215,6 +219,7 @@ void report_mismatches(World& w, const Options& o) {
 int run(World& w, const Options& o) {
   if (o.exchange_option >= 0) CHECK(lsb_set_option(w.ctx, o.exchange_option, 1));
   if (o.slices > 0) CHECK(lsb_set_option(w.ctx, LSB_OPT_EXCHANGE_SLICES, o.slices));
+  if (o.hybrid > 0) CHECK(lsb_set_option(w.ctx, LSB_OPT_HYBRID, o.hybrid));
   if (w.root()) {
     printf("Total number of HIP ranks: %d\n", w.P);
     printf("Problem size: %" PRId64 "\n", o.n);
@@ -367,6 +372,7 @@ int main(int argc, char* argv[]) {
     else if (a == "--radix-bits") o.radix_bits = std::stoi(next());
     else if (a == "--zipf-s") o.zipf_s = std::stod(next());
     else if (a == "--slices") o.slices = std::stoi(next());
+    else if (a == "--hybrid") o.hybrid = std::stoi(next());
     else if (a == "--test-corrupt") o.test_corrupt = std::stoll(next());
     else if (a == "--share-gpus") o.share_gpus = std::stoi(next());
     else if (a == "--exchange") {
@@ -385,7 +391,7 @@ int main(int argc, char* argv[]) {
   }
   if (!o.verify_set) o.verify = (o.n < 128LL * 1024 * 1024);
   if (o.radix_bits == 0) o.radix_bits = o.gpus > 1 ? 16 : 8;
-  if (o.n < 0 || o.ranks < 1 || o.gpus < 0 || o.share_gpus < 0) {
+  if (o.n < 0 || o.ranks < 1 || o.gpus < 0 || o.share_gpus < 0 || o.hybrid < 0 || o.hybrid > 2) {
     fprintf(stderr, "invalid arguments\n");
     return 2;
   }

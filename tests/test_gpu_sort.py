@@ -511,7 +511,8 @@ def test_beyond_32bit_indices(lsb_built):
 
 # ------------------------------------------------------------- the harness
 @pytest.mark.parametrize("extra", [[], ["--exchange", "peer"], ["--slices", "3", "--radix-bits", "16"],
-                                   ["--radix-bits", "64"]])
+                                   ["--radix-bits", "64"], ["--radix-bits", "64", "--hybrid", "1"],
+                                   ["--radix-bits", "64", "--hybrid", "2"]])
 def test_harness_matches_reference_lines(lsb_built, ref_vectors, extra):
     case = next(c for c in ref_vectors["cases"] if c["n"] == 1000003 and c["P"] == 4)
     exe = lsb_built.HARNESS_PATH
@@ -527,12 +528,19 @@ def test_harness_matches_reference_lines(lsb_built, ref_vectors, extra):
     assert printed == expect
 
 
-def test_harness_one_gpu_process(lsb_built):
+@pytest.mark.parametrize("extra", [[], ["--hybrid", "1"], ["--hybrid", "2"]])
+def test_harness_one_gpu_process(lsb_built, extra):
     exe = lsb_built.HARNESS_PATH
-    r = subprocess.run([exe, "--n", "300000", "--gpus", "1", "--verify", "--json"],
+    r = subprocess.run([exe, "--n", "300000", "--gpus", "1", "--verify", "--json"] + extra,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     assert "Array is sorted" in r.stdout
+
+
+def test_harness_rejects_bad_hybrid(lsb_built):
+    r = subprocess.run([lsb_built.HARNESS_PATH, "--n", "10", "--hybrid", "3"], capture_output=True,
+                       text=True, timeout=60)
+    assert r.returncode == 2
 
 
 # ------------------------------------------------ 16-bit digits (config C5)
