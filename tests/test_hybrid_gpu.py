@@ -127,6 +127,25 @@ def test_long_runs_take_the_segment_sort(lsb_built, oracle_mod):
     assert lp == 3 + 1  # 3 byte passes + the segmented sort
 
 
+@pytest.mark.parametrize("mids,run", [(28_000, 150), (20_000, 210)])
+def test_crossing_runs_past_one_window(lsb_built, oracle_mod, mids, run):
+    """Runs of ~150-210 records (equal on the two bytes below the top one):
+    k_segfix's 64-record windows do not hold the crossing run, so it scans on
+    (still under kSegCap): no k_segsort pass, output exact."""
+    rng = np.random.default_rng(mids)
+    n = 1 << 22
+    mid = rng.choice(1 << 16, mids, replace=False).astype(np.uint64)
+    a = np.zeros(n, dtype=DT)
+    a["key"] = ((rng.integers(0, 256, n, dtype=np.uint64) << np.uint64(56)) |
+                (mid[rng.integers(0, mid.size, n)] << np.uint64(40)) |
+                rng.integers(0, 1 << 40, n, dtype=np.uint64))
+    a["val"] = np.arange(n, dtype=np.uint64)
+    assert abs(n / np.unique(a["key"] >> np.uint64(40) & np.uint64(0xFFFF)).size - run) < run / 5
+    out, (lp, _, _), _ = _sort(lsb_built, a)
+    assert np.array_equal(out, oracle_mod.stable_sort(a))
+    assert lp == 3  # 3 byte passes, segments merged by k_segfix
+
+
 @pytest.mark.parametrize("bases", [1024, 4096])
 def test_long_segments_fall_back_to_lsd(lsb_built, oracle_mod, bases):
     """n / bases records share each of `bases` random top parts: the first
