@@ -2,8 +2,13 @@
 """Randomised stress of every sort form on one GPU: each iteration draws a
 size (1 .. 2^27 records, log-uniform, ragged), a rank count (P logical ranks,
 device-copy exchange), an exchange digit width (8, 16 or 64), a key
-distribution and a stage form, sorts, and checks lsb_verify and
-checkSorted.  Runs until --seconds have passed; one line per iteration.
+distribution, a stage form and a local-sort form (LSD or the hybrid's two
+modes), sorts, and checks lsb_verify and checkSorted.  One iteration in
+three instead sorts host-made keys (up to 2^22 records) whose bytes are
+thinned out at random -- constant bytes, few distinct values in the middle
+bytes, duplicates -- the inputs that take the hybrid's fallbacks and
+k_segfix's long crossing runs; those are checked against numpy's stable
+argsort.  Runs until --seconds have passed; one line per iteration.
 
     python tools/stress_mix.py --seconds 240 --seed 1
 """
@@ -16,6 +21,30 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "distributed-lsb_amd"))
 import lsbsort  # noqa: E402
+import numpy as np  # noqa: E402
+
+DT = np.dtype([("key", "<u8"), ("val", "<u8")])
+
+
+def thinned_keys(rng, n):
+    """Uniform keys with random structure: each byte kept, made constant, or
+    drawn from a small pool; sometimes whole keys from a small pool."""
+    g = np.random.default_rng(rng.randrange(1 << 30))
+    k = g.integers(0, 2**64 - 1, n, dtype=np.uint64)
+    for b in range(8):
+        r = rng.random()
+        sh = np.uint64(8 * b)
+        if r < 0.25:  # constant byte
+            k = (k & ~(np.uint64(0xFF) << sh)) | (np.uint64(rng.randrange(256)) << sh)
+        elif r < 0.45:  # few values
+            pool = g.integers(0, 256, rng.choice((2, 4, 16)), dtype=np.uint64)
+            k = (k & ~(np.uint64(0xFF) << sh)) | (pool[g.integers(0, pool.size, n)] << sh)
+    if rng.random() < 0.2:  # duplicates
+        k = k[g.integers(0, max(1, n // rng.choice((2, 8, 64))), n)]
+    a = np.zeros(n, dtype=DT)
+    a["key"] = k
+    a["val"] = np.arange(n, dtype=np.uint64)
+    return a
 
 
 def main():
@@ -33,13 +62,28 @@ def main():
         bits = rng.choice((8, 16, 64))
         dist = rng.choice(("uniform", "zipf"))
         split = rng.choice((0, 1, 2))
-        desc = f"iter {it}: n={n} P={P} bits={bits} dist={dist} split={split}"
+        hybrid = rng.choice((0, 1, 1, 2))
+        host = rng.random() < 1 / 3
+        if host:
+            n = min(n, 1 << 22)
+            dist = "thinned"
+        desc = f"iter {it}: n={n} P={P} bits={bits} dist={dist} split={split} hybrid={hybrid}"
         try:
             with lsbsort.World(n, ranks=P, radix_bits=bits) as w:
                 w.set_option(lsbsort.OPT_ONESWEEP_SPLIT, split)
-                w.generate(dist)
-                w.my_sort()
-                ok, first = w.verify()
+                w.set_option(lsbsort.OPT_HYBRID, hybrid)
+                if host:
+                    arr = thinned_keys(rng, n)
+                    w.scatter_global(arr)
+                    w.my_sort()
+                    got = w.gather_global()
+                    want = arr[np.argsort(arr["key"], kind="stable")]
+                    diff = np.nonzero(got != want)[0]
+                    ok, first = diff.size == 0, (int(diff[0]) if diff.size else -1)
+                else:
+                    w.generate(dist)
+                    w.my_sort()
+                    ok, first = w.verify()
                 srt = w.check_sorted()
         except lsbsort.LsbError as e:
             ok, first, srt = False, str(e), False
