@@ -209,17 +209,18 @@ __global__ __launch_bounds__(kSegBlock) __attribute__((amdgpu_waves_per_eu(LSB_S
 // LDS, and re-places only the records of buckets present on both sides:
 // slot = P - (left count) + #(keys < mine) + #(equal keys before me in the
 // input), over the few such records (~4 buckets of ~64 run records at
-// 2^30).  A run longer than kSegCap on one side, or one spanning a whole
-// tile (its segments then touch three tiles), sets *err: the runtime sorts
-// the segments with k_segsort instead.
+// 2^30).  A run longer than kSegCap on one side, one spanning a whole tile
+// (its segments then touch three tiles), or more than kSegCap records to
+// re-place sets *err: the runtime sorts the segments with k_segsort
+// instead.  16 KiB of LDS per 4 waves: 32 waves per CU.
 constexpr int kFixWaves = 4;  // boundaries per workgroup (one per wave)
 
 __global__ __launch_bounds__(64 * kFixWaves) void k_segfix(const Elem* __restrict__ in, Elem* __restrict__ out,
                                                            int64_t m, int shift, int64_t TT,
                                                            const uint32_t* __restrict__ status, SegPass seg) {
   __shared__ uint32_t cnt[kFixWaves][kBuckets];     // left count | right count << 16
-  __shared__ uint64_t mkey[kFixWaves][2 * kSegCap];  // the records to re-place: key,
-  __shared__ uint32_t mpos[kFixWaves][2 * kSegCap];  // and position in the run
+  __shared__ uint64_t mkey[kFixWaves][kSegCap];  // the records to re-place (at most
+  __shared__ uint32_t mpos[kFixWaves][kSegCap];  // kSegCap): key, position in the run
   const int w = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
   const uint64_t* __restrict__ K = reinterpret_cast<const uint64_t*>(in);
@@ -282,12 +283,18 @@ __global__ __launch_bounds__(64 * kFixWaves) void k_segfix(const Elem* __restric
       const uint64_t mb = __ballot(mv);
       if (mv) {
         const int q = nm + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mb, 0u));
-        mkey[w][q] = k;
-        mpos[w][q] = (uint32_t)x;
+        if (q < kSegCap) {
+          mkey[w][q] = k;
+          mpos[w][q] = (uint32_t)x;
+        }
       }
       nm += __popcll(mb);
     }
     wave_sync();
+    if (nm > kSegCap) {  // the same for the whole wave
+      bad = true;
+      continue;
+    }
     const int x_t = sub_of_tile(t, TT);
     for (int y = lane; y < nm; y += 64) {
       const uint64_t k = mkey[w][y];
