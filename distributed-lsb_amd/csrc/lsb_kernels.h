@@ -130,8 +130,9 @@ hipError_t onesweep_profile(unsigned long long* out10, bool reset);
 // rows and base (workgroup 0 writes base[x * 256 + b] = the first output slot
 // of bucket b's sub-array x records).  *err |= 1 when a segment inside a
 // tile holds more than kSegMax records, or a crossing run more than kSegCap
-// on one side of its boundary or spans a whole tile (the runtime then runs
-// k_segsort on the output).
+// (4 * kSegCap when runs average over 64 records) on one side of its
+// boundary or spans a whole tile (the runtime then runs k_segsort on the
+// output).
 constexpr int kSegCap = 256;
 struct SegPass {
   uint64_t pmask = 0;

@@ -209,18 +209,30 @@ __global__ __launch_bounds__(kSegBlock) __attribute__((amdgpu_waves_per_eu(LSB_S
 // LDS, and re-places only the records of buckets present on both sides:
 // slot = P - (left count) + #(keys < mine) + #(equal keys before me in the
 // input), over the few such records (~4 buckets of ~64 run records at
-// 2^30).  A run longer than kSegCap on one side, one spanning a whole tile
-// (its segments then touch three tiles), or more than kSegCap records to
-// re-place sets *err: the runtime sorts the segments with k_segsort
-// instead.  16 KiB of LDS per 4 waves: 32 waves per CU.
-constexpr int kFixWaves = 4;  // boundaries per workgroup (one per wave)
+// 2^30).  A run longer than CAP on one side, one spanning a whole tile (its
+// segments then touch three tiles), or more than CAP records to re-place
+// sets *err: the runtime sorts the segments with k_segsort instead.  The
+// records to re-place are grouped by bucket in LDS, so each ranks itself
+// against its own bucket's few.  Two shapes: CAP = kSegCap (256), one
+// 64-record chunk per side loaded up front, 20 KiB of LDS per 4 waves (32
+// waves per CU), when runs hold <= 64 records (m <= 2^30 at k = 4); and
+// CAP = 1024, four chunks per side, 28 KiB per 2 waves, for longer runs
+// (2^32 records: ~256 per run).
+__device__ __forceinline__ uint64_t lane0_u64(uint64_t x) {
+  return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32) |
+         (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)x);
+}
 
-__global__ __launch_bounds__(64 * kFixWaves) void k_segfix(const Elem* __restrict__ in, Elem* __restrict__ out,
-                                                           int64_t m, int shift, int64_t TT,
-                                                           const uint32_t* __restrict__ status, SegPass seg) {
-  __shared__ uint32_t cnt[kFixWaves][kBuckets];     // left count | right count << 16
-  __shared__ uint64_t mkey[kFixWaves][kSegCap];  // the records to re-place (at most
-  __shared__ uint32_t mpos[kFixWaves][kSegCap];  // kSegCap): key, position in the run
+// QW: 64-record chunks per side a boundary loads at once.
+template <int CAP, int WAVES, int QW>
+__global__ __launch_bounds__(64 * WAVES) void k_segfix(const Elem* __restrict__ in, Elem* __restrict__ out,
+                                                       int64_t m, int shift, int64_t TT,
+                                                       const uint32_t* __restrict__ status, SegPass seg) {
+  static_assert(CAP < 0x8000, "16-bit side counts");
+  __shared__ uint32_t cnt[WAVES][kBuckets];   // left count | right count << 16
+  __shared__ uint32_t moff[WAVES][kBuckets];  // a bucket's slice of mkey / mpos
+  __shared__ uint64_t mkey[WAVES][CAP];       // the records to re-place (at most
+  __shared__ uint32_t mpos[WAVES][CAP];       // CAP), by bucket: key, position in the run
   const int w = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
   const uint64_t* __restrict__ K = reinterpret_cast<const uint64_t*>(in);
@@ -230,80 +242,126 @@ __global__ __launch_bounds__(64 * kFixWaves) void k_segfix(const Elem* __restric
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   };
   bool bad = false;
-  for (int64_t t = (int64_t)blockIdx.x * kFixWaves + w; t + 1 < TT; t += (int64_t)gridDim.x * kFixWaves) {
+  for (int64_t t = (int64_t)blockIdx.x * WAVES + w; t + 1 < TT; t += (int64_t)gridDim.x * WAVES) {
     const int64_t b = (t + 1) * kTile;  // tile t + 1's first record
-    const uint64_t v = K[2 * (b - 1)] & seg.rmask;
-    if ((K[2 * b] & seg.rmask) != v) continue;  // the same for the whole wave
     const int64_t lo = t * kTile, hi = b + kTile < m ? b + kTile : m;
-    int a = 0, c = 0;  // the run's records before / from b, up to the two tiles' ends
-    for (;;) {
-      const int64_t i = b - 1 - a - lane;
-      const uint64_t stop = __ballot(!(i >= lo && (K[2 * i] & seg.rmask) == v));
-      if (stop) {
-        a += __builtin_ctzll(stop);
-        break;
-      }
-      a += 64;
-      if (a > kSegCap) break;
+    // The QW 64-record chunks on each side of b in one round trip: the
+    // boundary test, the run's extent and its keys (runs longer than that
+    // are scanned on and re-read from L2).
+    uint64_t kl[QW], kr[QW];
+#pragma unroll
+    for (int q = 0; q < QW; ++q) {
+      const int64_t il = b - 1 - 64 * q - lane, ir = b + 64 * q + lane;
+      kl[q] = il >= lo ? K[2 * il] : 0ull;
+      kr[q] = ir < hi ? K[2 * ir] : 0ull;
     }
-    for (;;) {
-      const int64_t i = b + c + lane;
-      const uint64_t stop = __ballot(!(i < hi && (K[2 * i] & seg.rmask) == v));
-      if (stop) {
-        c += __builtin_ctzll(stop);
-        break;
-      }
-      c += 64;
-      if (c > kSegCap) break;
+    const uint64_t v = lane0_u64(kl[0]) & seg.rmask;  // K[b - 1]
+    if ((lane0_u64(kr[0]) & seg.rmask) != v) continue;  // the same for the whole wave
+    int a = -1, c = -1;  // the run's records before / from b, up to the two tiles' ends
+#pragma unroll
+    for (int q = 0; q < QW; ++q) {
+      const int64_t il = b - 1 - 64 * q - lane, ir = b + 64 * q + lane;
+      const uint64_t sl = __ballot(!(il >= lo && (kl[q] & seg.rmask) == v));
+      const uint64_t sr = __ballot(!(ir < hi && (kr[q] & seg.rmask) == v));
+      if (a < 0 && sl) a = 64 * q + __builtin_ctzll(sl);
+      if (c < 0 && sr) c = 64 * q + __builtin_ctzll(sr);
     }
-    if (a > kSegCap || c > kSegCap || (b - a == lo && lo > 0 && (K[2 * (lo - 1)] & seg.rmask) == v) ||
+    const bool fast = a >= 0 && c >= 0;
+    if (a < 0) {
+      a = 64 * QW;
+      for (;;) {
+        const int64_t i = b - 1 - a - lane;
+        const uint64_t stop = __ballot(!(i >= lo && (K[2 * i] & seg.rmask) == v));
+        a += stop ? __builtin_ctzll(stop) : 64;
+        if (stop || a > CAP) break;
+      }
+    }
+    if (c < 0) {
+      c = 64 * QW;
+      for (;;) {
+        const int64_t i = b + c + lane;
+        const uint64_t stop = __ballot(!(i < hi && (K[2 * i] & seg.rmask) == v));
+        c += stop ? __builtin_ctzll(stop) : 64;
+        if (stop || c > CAP) break;
+      }
+    }
+    if (a > CAP || c > CAP || (b - a == lo && lo > 0 && (K[2 * (lo - 1)] & seg.rmask) == v) ||
         (b + c == hi && hi < m && (K[2 * hi] & seg.rmask) == v)) {
       bad = true;
       continue;
     }
     const int n = a + c;
     const int64_t r0 = b - a;
-    for (int d = lane; d < kBuckets; d += 64) cnt[w][d] = 0;
-    wave_sync();
-    for (int x = lane; x < n; x += 64) {
-      const uint32_t d = (uint32_t)(K[2 * (r0 + x)] >> shift) & (kBuckets - 1);
-      atomicAdd(&cnt[w][d], x < a ? 1u : 0x10000u);
-    }
-    wave_sync();
-    int nm = 0;  // records whose bucket has both sides: compacted in run order
-    for (int x0 = 0; x0 < n; x0 += 64) {
-      const int x = x0 + lane;
-      uint64_t k = 0;
-      bool mv = false;
-      if (x < n) {
-        k = K[2 * (r0 + x)];
-        const uint32_t cc = cnt[w][(uint32_t)(k >> shift) & (kBuckets - 1)];
-        mv = (cc & 0xFFFFu) != 0 && (cc >> 16) != 0;
-      }
-      const uint64_t mb = __ballot(mv);
-      if (mv) {
-        const int q = nm + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mb, 0u));
-        if (q < kSegCap) {
-          mkey[w][q] = k;
-          mpos[w][q] = (uint32_t)x;
+    // f(key, position in the run, valid) for every record of the run, 64 at
+    // a time (wave-uniform calls): from the registers, or from L2.
+    auto for_each = [&](auto&& f) {
+      if (fast) {
+#pragma unroll
+        for (int q = 0; q < QW; ++q) {
+          const int dist = 64 * q + lane;
+          f(kl[q], a - 1 - dist, dist < a);
+        }
+#pragma unroll
+        for (int q = 0; q < QW; ++q) {
+          const int p = 64 * q + lane;
+          f(kr[q], a + p, p < c);
+        }
+      } else {
+        for (int x0 = 0; x0 < n; x0 += 64) {
+          const int x = x0 + lane;
+          f(x < n ? K[2 * (r0 + x)] : 0ull, x, x < n);
         }
       }
-      nm += __popcll(mb);
-    }
+    };
+    for (int d = lane; d < kBuckets; d += 64) cnt[w][d] = 0;
     wave_sync();
-    if (nm > kSegCap) {  // the same for the whole wave
+    for_each([&](uint64_t k, int x, bool ok) {
+      if (ok) atomicAdd(&cnt[w][(uint32_t)(k >> shift) & (kBuckets - 1)], x < a ? 1u : 0x10000u);
+    });
+    wave_sync();
+    // The records to re-place (buckets with both sides), grouped by bucket:
+    // lane l owns buckets 4l..4l+3 and their slices' starts.
+    auto both = [](uint32_t cc) { return (cc & 0xFFFFu) && (cc >> 16) ? (cc & 0xFFFFu) + (cc >> 16) : 0u; };
+    uint32_t own = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) own += both(cnt[w][4 * lane + j]);
+    uint32_t incl = own;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t o = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += o;
+    }
+    const int nm = (int)__shfl(incl, 63, 64);
+    if (nm > CAP) {  // the same for the whole wave
       bad = true;
+      wave_sync();
       continue;
     }
+    uint32_t start = incl - own;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      moff[w][4 * lane + j] = start;
+      start += both(cnt[w][4 * lane + j]);
+    }
+    wave_sync();
+    for_each([&](uint64_t k, int x, bool ok) {
+      if (!ok) return;
+      const uint32_t d = (uint32_t)(k >> shift) & (kBuckets - 1);
+      if (!both(cnt[w][d])) return;
+      const uint32_t q = atomicAdd(&moff[w][d], 1u);  // any order: x breaks ties
+      mkey[w][q] = k;
+      mpos[w][q] = (uint32_t)x;
+    });
+    wave_sync();
     const int x_t = sub_of_tile(t, TT);
     for (int y = lane; y < nm; y += 64) {
       const uint64_t k = mkey[w][y];
       const uint32_t x = mpos[w][y];
       const uint32_t d = (uint32_t)(k >> shift) & (kBuckets - 1);
       uint32_t before = 0;
-      for (int z = 0; z < nm; ++z) {
+      const uint32_t z1 = moff[w][d];  // the end of bucket d's slice
+      for (uint32_t z = z1 - both(cnt[w][d]); z < z1; ++z) {
         const uint64_t kz = mkey[w][z];
-        if (((uint32_t)(kz >> shift) & (kBuckets - 1)) != d) continue;
         before += (kz < k || (kz == k && mpos[w][z] < x)) ? 1u : 0u;
       }
       const int64_t P = seg.base[x_t * kBuckets + d] + (int64_t)(status[t * kBuckets + d] & kStatusValMask);
@@ -324,8 +382,18 @@ hipError_t launch_segfix(const Elem* in, Elem* out, int64_t m, int shift, const 
   if (TT < 2) return hipSuccess;
   int64_t g = grid < 1 ? 1 : grid;
   if (g > TT - 1) g = TT - 1;
-  g = (g + kFixWaves - 1) / kFixWaves;
-  hipLaunchKernelGGL(k_segfix, dim3((unsigned)g), dim3(64 * kFixWaves), 0, s, in, out, m, shift, TT, status, seg);
+  // Records per run value: m over the run key's 2^bits values.
+  const int rbits = __builtin_popcountll(seg.rmask);
+  const int64_t rlen = rbits >= 62 ? 0 : m >> rbits;
+  if (rlen <= 64) {
+    g = (g + 3) / 4;
+    hipLaunchKernelGGL((k_segfix<kSegCap, 4, 1>), dim3((unsigned)g), dim3(256), 0, s, in, out, m, shift, TT,
+                       status, seg);
+  } else {
+    g = (g + 1) / 2;
+    hipLaunchKernelGGL((k_segfix<4 * kSegCap, 2, 4>), dim3((unsigned)g), dim3(128), 0, s, in, out, m, shift, TT,
+                       status, seg);
+  }
   return hipGetLastError();
 }
 

@@ -127,6 +127,17 @@ def test_long_runs_take_the_segment_sort(lsb_built, oracle_mod):
     assert lp == 3 + 1  # 3 byte passes + the segmented sort
 
 
+@pytest.mark.parametrize("n", [1 << 23, (1 << 23) + 4_097])
+def test_long_runs_take_the_large_segfix(lsb_built, oracle_mod, n):
+    """2^23 records over 3 top bytes: runs of ~128 records per value of the
+    two run bytes, so launch_segfix takes its 1024-record form; no k_segsort
+    pass, output exact."""
+    a = _uniform(n, 23)
+    out, (lp, _, _), rows = _sort(lsb_built, a, timing=True)
+    assert np.array_equal(out, oracle_mod.stable_sort(a))
+    assert lp == 3 and [r["shift"] for r in rows] == [40, 48, 56]
+
+
 @pytest.mark.parametrize("mids,run", [(28_000, 150), (20_000, 210)])
 def test_crossing_runs_past_one_window(lsb_built, oracle_mod, mids, run):
     """Runs of ~150-210 records (equal on the two bytes below the top one):

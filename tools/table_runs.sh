@@ -1,13 +1,15 @@
 #!/bin/bash
 # The DESIGN.md §4 bench table on one box: C2 default, reduce-then-scan,
-# Zipf keys, 16-bit digits, 2^32 records (bench.py lines in gpurun_out/table.log).
+# Zipf keys, 16-bit digits, 2^32 records, and the hybrid local sort at 2^30,
+# with Zipf keys and at 2^32 (bench.py lines in gpurun_out/table.log).
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd $R
 : > gpurun_out/table.log
-for args in "" "--passes reduce-scan" "--dist zipf" "--radix-bits 16" "--n-per-gpu 4294967296 --steps 3 --warmup 1"; do
+for args in "" "--passes reduce-scan" "--dist zipf" "--radix-bits 16" "--n-per-gpu 4294967296 --steps 3 --warmup 1" \
+    "--passes hybrid" "--passes hybrid --dist zipf" "--passes hybrid --n-per-gpu 4294967296 --steps 3 --warmup 1"; do
   echo "args: $args" >> gpurun_out/table.log
-  timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-traffic $args >> gpurun_out/table.log 2>&1 || exit 1
+  timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-traffic --no-extras $args >> gpurun_out/table.log 2>&1 || exit 1
 done
 python3 - <<'PY'
 import json
@@ -17,5 +19,8 @@ for line in open("gpurun_out/table.log"):
     elif line.startswith("{"):
         d = json.loads(line)
         r = d["roofline"]
-        print(f"{a:50s} {d['value']:10.1f} Melem/s {d['ms_per_step']:8.2f} ms  {r['kernel']} {r['avg_launch_ms']:.3f} ms frac {r['frac']:.3f}")
+        k = d.get("kernel_ms_per_step", {})
+        print(f"{a:50s} {d['value']:10.1f} Melem/s {d['ms_per_step']:8.2f} ms  {r['kernel']} {r['avg_launch_ms']:.3f} ms "
+              f"frac {r['frac']:.3f} verified {d['verified']} passes {d['config'].get('local_passes')} "
+              f"segsort {k.get('segsort', 0):.2f} ms")
 PY
