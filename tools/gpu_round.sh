@@ -1,6 +1,6 @@
 #!/bin/bash
 # One GPU check of the tree (run from the repo root on the GPU box):
-#   TAG=r03_v1 RUN="tests smoke bench n2 n4zipf torchrun profile sq" bash tools/gpu_round.sh
+#   TAG=r03_v1 RUN="tests smoke bench n2 n4zipf torchrun profile profhyb sq" bash tools/gpu_round.sh
 # Steps (each under its own time limit; the first failure ends the call):
 #   tests     the whole -m gpu suite
 #   smoke     __graft_entry__.smoke()
@@ -10,6 +10,8 @@
 #   n4zipf    the same at N = 4 with Zipf keys
 #   torchrun  bench.py --gpus 2 under torch.distributed.run (the driver's form)
 #   profile   tools/profile.sh: rocprofv3 stats + FETCH_SIZE / WRITE_SIZE passes
+#   profhyb   the same for bench.py --passes hybrid (gpurun_out/prof_hybrid;
+#             summarise with tools/pmc_summary.py TAG_hybrid gpurun_out/prof_hybrid ... --templates)
 #   sq        tools/sq_counters.sh: SQ counters of the sort at 2^28
 # Output under gpurun_out/$TAG/.
 set -o pipefail
@@ -52,6 +54,9 @@ for s in $RUN; do
     profile)
       bash tools/profile.sh > $O/profile.log 2>&1 || fail profile $O/profile.log
       cp $(find gpurun_out/prof/stats -name "*kernel_stats.csv" -print -quit) $O/kernel_stats.csv || true ;;
+    profhyb)
+      PROF=prof_hybrid BENCH_ARGS="--passes hybrid" bash tools/profile.sh > $O/profile_hybrid.log 2>&1 \
+        || fail profhyb $O/profile_hybrid.log ;;
     sq)
       SQ_TAG=_$TAG bash tools/sq_counters.sh > $O/sq.log 2>&1 || fail sq $O/sq.log ;;
     *) echo "unknown step $s"; exit 2 ;;
