@@ -140,11 +140,42 @@ struct SegPass {
   int64_t* base = nullptr;  // kOnesweepSubs * 256
   uint32_t* err = nullptr;
 };
+// Gathered input (per-digit exchange, LSB_OPT_EXCHANGE_GATHER): the pass
+// after an exchange reads its records where they arrived instead of from a
+// placed copy.  Position p of the placed order (the rank's block in
+// (digit, source) order) lies in piece e = b * P + s (bucket b's records from
+// source s), the last e with gstart[e] <= p; its record is
+//   R[p - place[s * nb + b]]                          (a peer's piece)
+//   A[p - place[s * nb + b] + self_adj]               (s == me, self_in_a)
+// TileDesc caches that per onesweep tile: up to 4 pieces (first position
+// relative to the tile, pointer adjustment, bit j of sel: piece j is in A);
+// n = kDescOverflow sends the tile's records to the search over [e0, e1].
+constexpr int kDescPieces = 4;
+constexpr int kDescOverflow = 0xFF;
+struct alignas(16) TileDesc {
+  int32_t n, e0, e1, sel;
+  int32_t start[kDescPieces];
+  int64_t adj[kDescPieces];
+};
+struct GatherSrc {
+  const Elem* R = nullptr;
+  const Elem* A = nullptr;
+  int64_t self_adj = 0;
+  const int64_t* place = nullptr;  // P * nb place_off (launch_plan)
+  const int64_t* gstart = nullptr;  // P * nb piece starts (launch_plan)
+  const int64_t* gadj = nullptr;    // P * nb scratch: 2 * pointer adjustment + (1: in A)
+  const TileDesc* desc = nullptr;   // onesweep_tiles(m)
+  int P = 1, nb = 256, me = 0, self_in_a = 1;
+};
+// gadj, then desc[t] for every onesweep tile of m records (after launch_plan
+// with gstart).
+hipError_t launch_gather_desc(const GatherSrc& g, int64_t m, TileDesc* desc, hipStream_t s);
 struct OnesweepExtra {
   uint64_t* totals = nullptr;
   uint64_t* count16 = nullptr;
   int halves = 1;  // 2: split stage, 3 workgroups per CU (skewed keys; not with count16)
   const SegPass* seg = nullptr;  // the hybrid's last pass (no next digit, whole stage)
+  const GatherSrc* gather = nullptr;  // records gathered from an exchange (`in` unused)
 };
 // The runtime's choice of OnesweepExtra::halves for a rank, from a digit's
 // sub-array histogram (kOnesweepSubs x 256 counts of m records): 2 when one
@@ -177,9 +208,11 @@ hipError_t launch_segfix(const Elem* in, Elem* out, int64_t m, int shift, const 
 // next_shift >= 0: also add the placed records' digit at next_shift to
 // next_hist[x * 256 + b] (x = the out position's onesweep sub-array over
 // out_len records; zeroed by the caller): the next local pass's sub_hist.
+// store = false (with next_shift >= 0): count only, out untouched (the next
+// pass gathers, GatherSrc).
 hipError_t launch_place(const Elem* src, Elem* out, int64_t out_len, int64_t k0, int64_t count,
                         int shift, int nbuckets, const int64_t* off_row, hipStream_t s,
-                        int next_shift = -1, uint32_t* next_hist = nullptr);
+                        int next_shift = -1, uint32_t* next_hist = nullptr, bool store = true);
 
 // Peer-store exchange (opt-in, LSB_OPT_EXCHANGE_PEER): from the all-gathered
 // counts hist[s * nb + b], rank `me` writes each of its m bucket-ordered
@@ -197,9 +230,12 @@ hipError_t launch_system_acquire(hipStream_t s);
 // hist[s * nb + b] (same rule as the host planner lsb_plan_exchange):
 // place[s * nb + b] = place_off, place[P * nb + s] = rend (inclusive scan of
 // recv counts), counts[0..P) = send counts, counts[P..2P) = recv counts.
-// work: P * nb int64, total: nb int64 scratch.
+// work: P * nb int64, total: nb int64 scratch.  gstart (optional, P * nb):
+// gstart[b * P + s] = first position of piece (b, s) in my block, clamped to
+// [0, here] (nondecreasing in b * P + s).
 hipError_t launch_plan(const uint64_t* hist, int P, int nb, int me, int64_t n, int64_t* work,
-                       int64_t* total, int64_t* place, int64_t* counts, hipStream_t s);
+                       int64_t* total, int64_t* place, int64_t* counts, hipStream_t s,
+                       int64_t* gstart = nullptr);
 
 // ---- whole-key exchange (radix_bits = 64; lsb_merge.hip) ----
 // Splitter search: for Q targets T_t, state[2t .. 2t+1] = key interval

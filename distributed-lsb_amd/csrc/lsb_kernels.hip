@@ -621,6 +621,28 @@ constexpr int kStPol = 16;
 typedef __attribute__((address_space(1))) uint32_t gu32;
 typedef uint32_t v2u __attribute__((ext_vector_type(2)));
 
+// Piece table of a gathered pass (GatherSrc): the last piece e in [e0, e1]
+// with gstart[e] <= p (the one holding placed position p), and its record.
+__device__ __forceinline__ int gather_piece(const GatherSrc& g, int e0, int e1, int64_t p) {
+  int lo = e0, hi = e1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (g.gstart[mid] <= p) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+// gadj[e] = 2 * (pointer adjustment of piece e) + (1: the piece is in A).
+__device__ __forceinline__ int64_t gather_adj(const GatherSrc& g, int e) {
+  const int src = e % g.P, b = e / g.P;
+  const bool in_a = src == g.me && g.self_in_a;
+  return 2 * ((in_a ? g.self_adj : 0) - g.place[(int64_t)src * g.nb + b]) + (in_a ? 1 : 0);
+}
+__device__ __forceinline__ const Elem* gather_search(const GatherSrc& g, int e0, int e1, int64_t p) {
+  const int64_t v = g.gadj[gather_piece(g, e0, e1, p)];
+  return ((v & 1) ? g.A : g.R) + (p + (v >> 1));
+}
+
 // sub_first_tile, sub_of_tile: lsb_device.h
 
 // sub_hist[x * 256 + b] += number of records of sub-array x with digit b;
@@ -763,13 +785,20 @@ __device__ unsigned long long g_os_prof[10];
 // look-back rows and the bucket bases workgroup 0 writes to seg.base: the
 // pass records nothing per tile (crossing-run lists appended here cost it
 // ~1 ms at 2^30, profiles/r03_ab_seg.log).
-template <int BLOCK, int IPT, bool NEXT, bool C16, int HALVES, bool SEG = false>
+//
+// GATHER (the pass after a per-digit exchange, LSB_OPT_EXCHANGE_GATHER): the
+// tile's records are read where the exchange left them (GatherSrc: the
+// receive buffer, and the rank's own segment in A) instead of from a placed
+// copy.  Wave 0 fetches the next tile's TileDesc while this tile is written,
+// so the loads at the loop top wait on nothing new; a tile of more than
+// kDescPieces pieces searches the piece table per record.
+template <int BLOCK, int IPT, bool NEXT, bool C16, int HALVES, bool SEG = false, bool GATHER = false>
 __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_onesweep(
     const Elem* __restrict__ in, Elem* __restrict__ out, int64_t m, int shift, int next_shift,
     const uint32_t* __restrict__ sub_hist, uint32_t* __restrict__ next_hist,
     uint32_t* __restrict__ status, uint32_t* __restrict__ tile_ctr, uint32_t epoch,
     uint32_t* __restrict__ err, uint64_t* __restrict__ totals,
-    unsigned long long* __restrict__ count16, SegPass seg) {
+    unsigned long long* __restrict__ count16, SegPass seg, GatherSrc gs) {
   constexpr int W = BLOCK / 64;
   constexpr int T = BLOCK * IPT;
   static_assert(!SEG || (!NEXT && !C16 && HALVES == 1), "the segment pass: last pass, whole stage");
@@ -790,6 +819,7 @@ __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_
   __shared__ uint32_t scan32[W];
   __shared__ int32_t s_tile, s_sub;
   __shared__ uint32_t tile_lo[2];  // C16: low byte of the tile's first, last record
+  __shared__ TileDesc s_desc;      // GATHER: where this tile's records are
 
   const int t = threadIdx.x;
   const bool bkt = BLOCK == kBuckets || t < kBuckets;  // a bucket thread
@@ -870,12 +900,22 @@ __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_
   // (a device-scope atomic is ~1 us under load; 3 % of the sort, measured).
   int nxt_tile = -1, nxt_sub = 0;
   if (t == 0) grab(nxt_tile, nxt_sub);
+  // GATHER: lanes 0-3 of wave 0 hold the next tile's descriptor.
+  uint4 dreg = make_uint4(0u, 0u, 0u, 0u);
+  auto fetch_desc = [&]() {
+    if (GATHER && w == 0) {
+      const int nt = __builtin_amdgcn_readfirstlane(nxt_tile);
+      if (nt >= 0 && lane < 4) dreg = reinterpret_cast<const uint4*>(gs.desc + nt)[lane];
+    }
+  };
+  fetch_desc();
 
   for (;;) {
     if (t == 0) {
       s_tile = nxt_tile;
       s_sub = nxt_sub;
     }
+    if (GATHER && w == 0 && lane < 4) reinterpret_cast<uint4*>(&s_desc)[lane] = dreg;
 #pragma unroll
     for (int j = 0; j < kBuckets / 64; ++j) wcnt[w][lane + 64 * j] = 0;
     __syncthreads();
@@ -896,10 +936,47 @@ __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_
 
     Elem e[IPT];
     const int wbase = w * 64 * IPT + (int)lane;
+    if (GATHER) {
+      const int dn = __builtin_amdgcn_readfirstlane(s_desc.n);
+      if (dn != kDescOverflow) {
+        // The pieces' base pointers and first tile positions are uniform
+        // (scalar registers); a record picks its piece by compares.
+        const uint32_t sel = (uint32_t)__builtin_amdgcn_readfirstlane(s_desc.sel);
+        const Elem* pb[kDescPieces];
+        int st[kDescPieces];
 #pragma unroll
-    for (int i = 0; i < IPT; ++i) {
-      const int li = wbase + i * 64;
-      e[i] = li < nvalid ? load_elem_nt(in + tb + li) : Elem{0ull, 0ull};
+        for (int k = 0; k < kDescPieces; ++k) {
+          st[k] = __builtin_amdgcn_readfirstlane(s_desc.start[k]);
+          const uint64_t a = s_desc.adj[k];
+          const int64_t adj = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(a >> 32)) << 32) |
+                                        (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a));
+          pb[k] = ((sel >> k) & 1u ? gs.A : gs.R) + (tb + adj);
+        }
+#pragma unroll
+        for (int i = 0; i < IPT; ++i) {
+          const int li = wbase + i * 64;
+          const Elem* src = pb[0];
+#pragma unroll
+          for (int k = 1; k < kDescPieces; ++k) src = li >= st[k] ? pb[k] : src;
+          e[i] = li < nvalid ? load_elem_nt(src + li) : Elem{0ull, 0ull};
+        }
+      } else {
+        // One record's search at a time (the scheduling barrier keeps the
+        // compiler from interleaving 8 searches, which would spill).
+        const int e0 = s_desc.e0, e1 = s_desc.e1;
+#pragma unroll
+        for (int i = 0; i < IPT; ++i) {
+          const int li = wbase + i * 64;
+          e[i] = li < nvalid ? load_elem_nt(gather_search(gs, e0, e1, tb + li)) : Elem{0ull, 0ull};
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < IPT; ++i) {
+        const int li = wbase + i * 64;
+        e[i] = li < nvalid ? load_elem_nt(in + tb + li) : Elem{0ull, 0ull};
+      }
     }
 #ifdef LSB_OS_PROFILE
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1177,6 +1254,8 @@ __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_
           ++acc;
         }
       }
+      // After wave 0's writes: the grab has returned by then.
+      if (h == HALVES - 1) fetch_desc();
       __syncthreads();
     }
     OS_MARK(4);  // write
@@ -1209,7 +1288,11 @@ constexpr int kPlaceNextGrid = 1024;    // k_place<., kNext> grid cap (one flush
 // added to next_hist at the end: the next pass's sub_hist, so that pass
 // needs no count read (k_subhist).  The exchange launches one k_place per
 // (source, slice); they all add into one next_hist.
-template <bool kLds, bool kNext>
+//
+// kStore = false (LSB_OPT_EXCHANGE_GATHER): the count alone; the next pass
+// gathers its tiles from where the records arrived (GatherSrc), so the
+// placement's 16 B per record of writes go.
+template <bool kLds, bool kNext, bool kStore = true>
 __global__ __launch_bounds__(kPlaceBlock) void k_place(const Elem* __restrict__ src,
                                                        Elem* __restrict__ out, int64_t k0,
                                                        int64_t count, int shift, uint32_t mask,
@@ -1246,7 +1329,7 @@ __global__ __launch_bounds__(kPlaceBlock) void k_place(const Elem* __restrict__ 
         const uint32_t d = (uint32_t)(x[i].key >> shift) & mask;
         const int64_t g = off[d] + k0 + k;
         LSB_DASSERT(g >= 0 && g < out_len);
-        store_elem(out + g, x[i]);
+        if (kStore) store_elem(out + g, x[i]);
         if (kNext) {
           const uint32_t xs = (uint32_t)sub_of_tile(g / kTile, TT);
           atomicAdd(&nh[xs * kBuckets + ((uint32_t)(x[i].key >> next_shift) & (kBuckets - 1))], 1u);
@@ -1498,7 +1581,8 @@ __global__ __launch_bounds__(256) void k_plan_pieces(const uint64_t* __restrict_
                                                      const int64_t* __restrict__ base,
                                                      int64_t* __restrict__ work,
                                                      int64_t* __restrict__ place,
-                                                     unsigned long long* __restrict__ send_counts) {
+                                                     unsigned long long* __restrict__ send_counts,
+                                                     int64_t* __restrict__ gstart) {
   // Send counts are summed per workgroup in LDS first: every bucket of a
   // rank adds to the same few owners, and 65536 same-address global
   // atomics took 0.8 ms.
@@ -1516,6 +1600,10 @@ __global__ __launch_bounds__(256) void k_plan_pieces(const uint64_t* __restrict_
     const int64_t phi = g1 < hi ? g1 : hi;
     work[i] = phi > plo ? phi - plo : 0;  // piece length
     place[i] = plo;                       // piece's first dest (if any)
+    if (gstart) {  // (b, s) order: the placed order of my block
+      const int64_t l = g0 < lo ? 0 : (g0 > hi ? hi - lo : g0 - lo);
+      gstart[(int64_t)b * P + s] = l;
+    }
     if (s == me && h > 0) {
       int64_t g = g0;
       while (g < g1) {  // split my run over its owners
@@ -1554,6 +1642,53 @@ __global__ __launch_bounds__(256) void k_plan_finish(int P, int nb, int64_t lo,
   int64_t displ = 0;
   for (int q = 0; q < s; ++q) displ += recv_counts[q];
   place[i] = (place[i] - lo) - (displ + work[i]);
+}
+
+__global__ __launch_bounds__(256) void k_gather_adj(GatherSrc g, int64_t* __restrict__ gadj) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e < (int64_t)g.P * g.nb) gadj[e] = gather_adj(g, (int)e);
+}
+
+// Tile descriptors of a gathered pass: tile t's pieces (at most kDescPieces,
+// else kDescOverflow and the per-record search over [e0, e1]).
+__global__ __launch_bounds__(256) void k_gather_desc(GatherSrc g, int64_t m, int64_t TT,
+                                                     TileDesc* __restrict__ desc) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= TT) return;
+  const int cells = g.P * g.nb;
+  const int64_t tb = t * kTile;
+  const int64_t te = (tb + kTile < m ? tb + kTile : m) - 1;
+  const int e0 = gather_piece(g, 0, cells - 1, tb);
+  const int e1 = gather_piece(g, e0, cells - 1, te);
+  TileDesc d;
+  d.e0 = e0;
+  d.e1 = e1;
+  d.sel = 0;
+  int n = 0;
+#pragma unroll
+  for (int k = 0; k < kDescPieces; ++k) {
+    d.start[k] = 0x7FFFFFFF;
+    d.adj[k] = 0;
+  }
+  if (e1 - e0 < 64) {
+    for (int e = e0; e <= e1; ++e) {
+      const int64_t st = g.gstart[e], en = e + 1 < cells ? g.gstart[e + 1] : m;
+      if (en <= st) continue;  // empty piece
+      if (n == kDescPieces) {
+        n = kDescOverflow;
+        break;
+      }
+      const int64_t v = gather_adj(g, e);
+      d.start[n] = st > tb ? (int32_t)(st - tb) : 0;
+      d.adj[n] = v >> 1;
+      d.sel |= (int)(v & 1) << n;
+      ++n;
+    }
+  } else {
+    n = kDescOverflow;
+  }
+  d.n = n;
+  desc[t] = d;
 }
 
 // ------------------------------------------------------------------ checks
@@ -1737,46 +1872,53 @@ hipError_t launch_onesweep(const Elem* in, Elem* out, int64_t m, int shift, int 
   if (g > (TT + kSub - 1) / kSub * kSub) g = (TT + kSub - 1) / kSub * kSub;
   const dim3 gd((unsigned)g), bd(split ? kOsSplitBlock : kOsBlock);
   uint32_t* st = status;
+  const GatherSrc gsrc = extra.gather ? *extra.gather : GatherSrc();
+  const bool gat = extra.gather != nullptr;
+  // One launch of the instance, gathered or not.
+  auto go = [&](auto kplain, auto kgather, int nshift, uint32_t* nhist, unsigned long long* cnt16,
+                SegPass sp) {
+    hipLaunchKernelGGL(gat ? kgather : kplain, gd, bd, 0, s, in, out, m, shift, nshift, sub_hist, nhist,
+                       st, tile_ctr, epoch, err, extra.totals, cnt16, sp, gsrc);
+  };
   if (extra.seg) {
     // The hybrid's last pass: no next digit, no 16-bit counts, whole stage.
     if (next_shift >= 0 || c16 || extra.halves != 1 || !extra.seg->base ||
-        !extra.seg->err)
+        !extra.seg->err || gat)
       return hipErrorInvalidValue;
     hipLaunchKernelGGL((k_onesweep<kOsBlock, kOsIpt, false, false, 1, true>), gd, bd, 0, s, in, out, m,
                        shift, 0, sub_hist, nullptr, st, tile_ctr, epoch, err, extra.totals, nullptr,
-                       *extra.seg);
+                       *extra.seg, gsrc);
   } else if (c16) {
     // The 16-bit counts need the low byte below this digit, and no next
     // digit: the exchange follows this pass.
     if (shift < 8 || next_shift >= 0) return hipErrorInvalidValue;
     e = hipMemsetAsync(c16, 0, sizeof(uint64_t) * 65536, s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_onesweep<kOsBlock, kOsIpt, false, true, 1>), gd, bd, 0, s, in, out,
-                       m, shift, 0, sub_hist, nullptr, st, tile_ctr, epoch, err, extra.totals, c16, SegPass());
+    go(k_onesweep<kOsBlock, kOsIpt, false, true, 1>, k_onesweep<kOsBlock, kOsIpt, false, true, 1, false, true>,
+       0, nullptr, c16, SegPass());
   } else if (next_shift >= 0) {
     e = hipMemsetAsync(next_hist, 0, sizeof(uint32_t) * kSub * kBuckets, s);
     if (e != hipSuccess) return e;
     if (split)
-      hipLaunchKernelGGL((k_onesweep<kOsSplitBlock, kOsSplitIpt, true, false, 2>), gd, bd, 0, s, in, out,
-                         m, shift, next_shift, sub_hist, next_hist, st, tile_ctr, epoch, err,
-                         extra.totals, nullptr, SegPass());
+      go(k_onesweep<kOsSplitBlock, kOsSplitIpt, true, false, 2>,
+         k_onesweep<kOsSplitBlock, kOsSplitIpt, true, false, 2, false, true>, next_shift, next_hist, nullptr,
+         SegPass());
     else
-      hipLaunchKernelGGL((k_onesweep<kOsBlock, kOsIpt, true, false, 1>), gd, bd, 0, s, in, out,
-                         m, shift, next_shift, sub_hist, next_hist, st, tile_ctr, epoch, err,
-                         extra.totals, nullptr, SegPass());
+      go(k_onesweep<kOsBlock, kOsIpt, true, false, 1>, k_onesweep<kOsBlock, kOsIpt, true, false, 1, false, true>,
+         next_shift, next_hist, nullptr, SegPass());
   } else if (split) {
-    hipLaunchKernelGGL((k_onesweep<kOsSplitBlock, kOsSplitIpt, false, false, 2>), gd, bd, 0, s, in, out,
-                       m, shift, 0, sub_hist, nullptr, st, tile_ctr, epoch, err, extra.totals, nullptr, SegPass());
+    go(k_onesweep<kOsSplitBlock, kOsSplitIpt, false, false, 2>,
+       k_onesweep<kOsSplitBlock, kOsSplitIpt, false, false, 2, false, true>, 0, nullptr, nullptr, SegPass());
   } else {
-    hipLaunchKernelGGL((k_onesweep<kOsBlock, kOsIpt, false, false, 1>), gd, bd, 0, s, in, out,
-                       m, shift, 0, sub_hist, nullptr, st, tile_ctr, epoch, err, extra.totals, nullptr, SegPass());
+    go(k_onesweep<kOsBlock, kOsIpt, false, false, 1>, k_onesweep<kOsBlock, kOsIpt, false, false, 1, false, true>,
+       0, nullptr, nullptr, SegPass());
   }
   return hipGetLastError();
 }
 
 hipError_t launch_place(const Elem* src, Elem* out, int64_t out_len, int64_t k0, int64_t count,
                         int shift, int nbuckets, const int64_t* off_row, hipStream_t s,
-                        int next_shift, uint32_t* next_hist) {
+                        int next_shift, uint32_t* next_hist, bool store) {
   if (count <= 0) return hipSuccess;
   if (nbuckets != 256 && nbuckets != 65536) return hipErrorInvalidValue;
   if (k0 < 0 || k0 + count > out_len) return hipErrorInvalidValue;
@@ -1786,6 +1928,15 @@ hipError_t launch_place(const Elem* src, Elem* out, int64_t out_len, int64_t k0,
     if (next_shift > 56 || !next_hist || out_len > kOnesweepMaxElems) return hipErrorInvalidValue;
     // Fewer, longer-lived workgroups: each flushes its 8 x 256 counters once.
     const dim3 grid(grid_for(count, kPlaceBlock * kPlaceIpt, kPlaceNextGrid));
+    if (!store) {
+      if (lds)
+        hipLaunchKernelGGL((k_place<true, true, false>), grid, dim3(kPlaceBlock), 0, s, src, out, k0,
+                           count, shift, mask, off_row, out_len, next_shift, next_hist);
+      else
+        hipLaunchKernelGGL((k_place<false, true, false>), grid, dim3(kPlaceBlock), 0, s, src, out, k0,
+                           count, shift, mask, off_row, out_len, next_shift, next_hist);
+      return hipGetLastError();
+    }
     if (lds)
       hipLaunchKernelGGL((k_place<true, true>), grid, dim3(kPlaceBlock), 0, s, src, out, k0, count,
                          shift, mask, off_row, out_len, next_shift, next_hist);
@@ -1794,6 +1945,7 @@ hipError_t launch_place(const Elem* src, Elem* out, int64_t out_len, int64_t k0,
                          shift, mask, off_row, out_len, next_shift, next_hist);
     return hipGetLastError();
   }
+  if (!store) return hipErrorInvalidValue;  // nothing to count
   const dim3 grid(grid_for(count, kPlaceBlock * kPlaceIpt, 4096));
   if (lds)
     hipLaunchKernelGGL((k_place<true, false>), grid, dim3(kPlaceBlock), 0, s, src, out, k0, count,
@@ -1830,7 +1982,8 @@ hipError_t launch_system_acquire(hipStream_t s) {
 }
 
 hipError_t launch_plan(const uint64_t* hist, int P, int nb, int me, int64_t n, int64_t* work,
-                       int64_t* total, int64_t* place, int64_t* counts, hipStream_t s) {
+                       int64_t* total, int64_t* place, int64_t* counts, hipStream_t s,
+                       int64_t* gstart) {
   if (P < 1 || me < 0 || me >= P || nb < 1 || n < 0) return hipErrorInvalidValue;
   const int64_t per = (n + P - 1) / P;
   const int64_t lo = (int64_t)me * per;
@@ -1845,10 +1998,23 @@ hipError_t launch_plan(const uint64_t* hist, int P, int nb, int me, int64_t n, i
   hipLaunchKernelGGL(k_plan_base, dim3(1), dim3(kPlanScanBlock), 0, s, total, nb);
   hipLaunchKernelGGL(k_plan_pieces, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, s, hist, P,
                      nb, me, per, lo, hi, total, work, place,
-                     reinterpret_cast<unsigned long long*>(counts));
+                     reinterpret_cast<unsigned long long*>(counts), gstart);
   hipLaunchKernelGGL(k_plan_rows, dim3(P), dim3(kPlanScanBlock), 0, s, work, nb, counts + P);
   hipLaunchKernelGGL(k_plan_finish, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, s, P, nb,
                      lo, work, counts + P, place);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_desc(const GatherSrc& g, int64_t m, TileDesc* desc, hipStream_t s) {
+  if (m <= 0) return hipSuccess;
+  if (!g.R || !g.A || !g.place || !g.gstart || !g.gadj || !desc || g.P < 1 || g.me < 0 || g.me >= g.P ||
+      (g.nb != 256 && g.nb != 65536) || (int64_t)g.P * g.nb > (int64_t(1) << 30))
+    return hipErrorInvalidValue;
+  const int64_t TT = (m + kTile - 1) / kTile;
+  const int64_t cells = (int64_t)g.P * g.nb;
+  hipLaunchKernelGGL(k_gather_adj, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, s, g,
+                     const_cast<int64_t*>(g.gadj));
+  hipLaunchKernelGGL(k_gather_desc, dim3((unsigned)((TT + 255) / 256)), dim3(256), 0, s, g, m, TT, desc);
   return hipGetLastError();
 }
 

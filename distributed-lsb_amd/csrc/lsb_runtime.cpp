@@ -108,6 +108,15 @@ struct Rank {
   int place_next = -1;
   uint32_t* place_hist = nullptr;
   bool counts_ready = false;            // totals16 = this exchange digit's counts (k_onesweep C16)
+  // Gathered passes (LSB_OPT_EXCHANGE_GATHER): an exchange whose placement
+  // only counts leaves the peers' records in R and the rank's own in A; the
+  // next local pass reads them there through gsrc (piece starts in gstart,
+  // one descriptor per onesweep tile in gdesc), allocated on first use.
+  bool gather_next = false;             // this exchange counts only
+  bool gather_pending = false;          // the next local pass gathers
+  int64_t* gstart = nullptr;            // [nb][P] piece starts in the placed order
+  lsb::TileDesc* gdesc = nullptr;       // [tiles]
+  lsb::GatherSrc gsrc;
   // Whole-key exchange (radix_bits = 64), allocated on first use.
   uint64_t* split_state = nullptr;      // [Q][2] key interval per target
   int64_t* split_targets = nullptr;     // [Q] global positions q * per
@@ -144,6 +153,7 @@ struct lsb_ctx {
   bool peer_ready = false;    // peer tables set up
   bool onesweep = true;       // P == 1: single-read passes (k_subhist + k_onesweep)
   bool self_coll = false;     // the self segment also goes through the collective
+  bool gather = true;         // LSB_OPT_EXCHANGE_GATHER: count-only placement + gathered pass
   int os_split = 0;           // LSB_OPT_ONESWEEP_SPLIT: 0 auto, 1 never, 2 always
   int hybrid = 0;             // LSB_OPT_HYBRID: 0 off, 1 k byte passes (the last one
                               // ordering segments, + k_segfix), 2 the same + a k_segsort pass
@@ -365,6 +375,8 @@ void free_rank(Rank& r) {
   (void)hipHostFree(r.split_h);
   (void)hipFree(r.merge_path);
   (void)hipFree(r.os_status);
+  (void)hipFree(r.gstart);
+  (void)hipFree(r.gdesc);
   (void)hipFree(r.seg_base);
   (void)hipFree(r.os_hist);
   (void)hipFree(r.os_ctr);
@@ -464,10 +476,14 @@ int digit_counts(lsb_ctx* c, Rank& r, int digit, const uint64_t** counts) {
 // back (RCCL takes host counts).  Call plan_fetch after a stream sync.
 int plan_launch(lsb_ctx* c, Rank& r) {
   HIP_TRY(hipSetDevice(r.dev));
+  if (r.gather_next && !r.gstart) {
+    LSB_TRY(dev_alloc(&r.gstart, (size_t)2 * c->P * c->nb));  // gstart, then gadj
+    LSB_TRY(dev_alloc(&r.gdesc, (size_t)lsb::onesweep_tiles(r.here)));
+  }
   {
     Timer t(c, &r, LSB_K_EXCHANGE);
     HIP_TRY(lsb::launch_plan(r.gather, c->P, c->nb, r.rank, c->n, r.plan_work, r.plan_total,
-                             r.place, r.plan_counts, r.stream));
+                             r.place, r.plan_counts, r.stream, r.gather_next ? r.gstart : nullptr));
   }
   HIP_TRY(hipMemcpyAsync(r.counts_h, r.plan_counts, sizeof(int64_t) * 2 * c->P,
                          hipMemcpyDeviceToHost, r.stream));
@@ -497,6 +513,13 @@ int64_t part(int64_t n, int j, int slices) { return n * j / slices; }
 // slice's merge (ceil(log2 P) levels) is the tail after the wire goes quiet.
 int slices_of(const lsb_ctx* c) { return c->slices > 0 ? c->slices : (c->bits == 64 ? 8 : 4); }
 
+// After an exchange's placements: B holds the placed block and becomes A, or
+// (count-only placement) the next pass gathers from R and A.
+void end_placement(Rank& r) {
+  if (r.gather_next) r.gather_pending = true;
+  else std::swap(r.A, r.B);
+}
+
 // Everything after this on r.stream waits for r.pstream's work so far.
 int join_place(Rank& r) {
   HIP_TRY(hipEventRecord(r.pdone, r.pstream));
@@ -511,7 +534,7 @@ int place_range(lsb_ctx* c, Rank& r, int shift, int src_rank, const Elem* src, i
   Timer t(c, &r, LSB_K_PLACE, r.pstream);
   HIP_TRY(lsb::launch_place(src, r.B, r.here, k0, cnt, shift, c->nb,
                             r.place + (size_t)src_rank * c->nb, r.pstream, r.place_next,
-                            r.place_hist));
+                            r.place_hist, !r.gather_next));
   return LSB_OK;
 }
 
@@ -531,6 +554,23 @@ int place_self(lsb_ctx* c, Rank& r, int shift) {
   if (r.send_counts[me] != r.recv_counts[me])
     return fail(LSB_ERR_STATE, "exchange", "self count mismatch");
   LSB_TRY(ensure_recv(c, r));
+  if (r.gather_next) {  // where the next pass will find each tile's records
+    lsb::GatherSrc& g = r.gsrc;
+    g.R = r.R;
+    g.A = r.A;
+    g.self_adj = r.send_displs[me] - r.recv_displs[me];
+    g.place = r.place;
+    g.gstart = r.gstart;
+    g.gadj = r.gstart + (size_t)c->P * c->nb;
+    g.desc = r.gdesc;
+    g.P = c->P;
+    g.nb = c->nb;
+    g.me = me;
+    g.self_in_a = !(c->self_coll && c->mode != Mode::kLoopback);
+    HIP_TRY(hipSetDevice(r.dev));
+    Timer t(c, &r, LSB_K_EXCHANGE);
+    HIP_TRY(lsb::launch_gather_desc(g, r.here, r.gdesc, r.stream));
+  }
   if (c->self_coll && c->mode != Mode::kLoopback) return LSB_OK;
   HIP_TRY(hipSetDevice(r.dev));
   HIP_TRY(hipEventRecord(r.pevent, r.stream));  // plan kernels done
@@ -608,7 +648,7 @@ int exchange_loopback(lsb_ctx* c, int digit) {
   for (Rank& r : c->ranks) {
     LSB_TRY(join_place(r));
     HIP_TRY(hipStreamSynchronize(r.stream));
-    std::swap(r.A, r.B);
+    end_placement(r);
   }
   return LSB_OK;
 }
@@ -866,7 +906,7 @@ int exchange_rccl(lsb_ctx* c, int digit) {
     LSB_TRY(place_slice(c, r, shift, j));
   }
   LSB_TRY(join_place(r));
-  std::swap(r.A, r.B);
+  end_placement(r);
   return LSB_OK;
 }
 
@@ -1257,11 +1297,19 @@ int local_pass_os(lsb_ctx* c, Rank& r, int shift, int next, lsb::OnesweepExtra e
     return LSB_OK;
   }
   uint32_t* hist[2] = {r.os_hist, r.os_hist + lsb::kOnesweepSubs * lsb::kBuckets};
-  if (r.os_valid != shift) {  // nothing counted this byte over A: read it
+  if (r.gather_pending) {  // the exchange's count-only placement counted this byte
+    if (r.os_valid != shift) {
+      r.gather_pending = false;
+      return fail(LSB_ERR_STATE, "local_pass_os", "gathered pass without its count");
+    }
+    extra.gather = &r.gsrc;
+  } else if (r.os_valid != shift) {  // nothing counted this byte over A: read it
     Timer t(c, &r, LSB_K_UPSWEEP);
     HIP_TRY(lsb::launch_subhist(r.A, m, shift, r.os_grid, hist[r.os_cur], nullptr, r.stream));
   }
-  LSB_TRY(onesweep_launch(c, r, shift, next, hist[r.os_cur], hist[r.os_cur ^ 1], extra));
+  const int rc = onesweep_launch(c, r, shift, next, hist[r.os_cur], hist[r.os_cur ^ 1], extra);
+  r.gather_pending = false;
+  LSB_TRY(rc);
   if (next >= 0) {
     r.os_cur ^= 1;
     r.os_valid = next;
@@ -1352,6 +1400,7 @@ int sort_exchange_onesweep(lsb_ctx* c) {
     if (!st.exch) continue;
     for (Rank& r : c->ranks) {
       r.place_next = c->peer || r.here == 0 ? -1 : after;
+      r.gather_next = c->gather && r.place_next >= 0;
       r.place_hist = nullptr;
       if (r.place_next >= 0) {
         r.place_hist = r.os_hist + (size_t)(r.os_cur ^ 1) * lsb::kOnesweepSubs * lsb::kBuckets;
@@ -1372,6 +1421,8 @@ int sort_exchange_onesweep(lsb_ctx* c) {
       r.place_next = -1;
       r.place_hist = nullptr;
       r.counts_ready = false;
+      r.gather_next = false;
+      if (rc != LSB_OK) r.gather_pending = false;
     }
     LSB_TRY(rc);
   }
@@ -2038,6 +2089,9 @@ int lsb_set_option(lsb_ctx_t* c, int option, int64_t value) {
       return LSB_OK;
     case LSB_OPT_EXCHANGE_SELF:
       c->self_coll = value != 0;
+      return LSB_OK;
+    case LSB_OPT_EXCHANGE_GATHER:
+      c->gather = value != 0;
       return LSB_OK;
     case LSB_OPT_HYBRID:
       if (value < 0 || value > 2) return fail(LSB_ERR_INVALID, "lsb_set_option", "hybrid must be 0, 1 or 2");

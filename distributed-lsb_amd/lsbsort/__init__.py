@@ -51,6 +51,7 @@ OPT_ONESWEEP = 6
 OPT_EXCHANGE_SELF = 7
 OPT_ONESWEEP_SPLIT = 8
 OPT_HYBRID = 9
+OPT_EXCHANGE_GATHER = 10
 MAX_PASSES = 16
 
 

@@ -115,6 +115,14 @@ typedef struct lsb_ctx lsb_ctx_t;
                                       take k_segsort, and segments longer than 1024 records make
                                       the sort redo the kept input by the LSD passes.  Needs a
                                       third record buffer. */
+#define LSB_OPT_EXCHANGE_GATHER 10 /* per-digit exchange forms with single-read local passes:
+                                      1 (default) every exchange but the last only counts
+                                      the next byte as the records arrive, and the next local
+                                      pass reads its tiles from where they arrived (the
+                                      receive buffer, the rank's own segment in A) through
+                                      the plan's piece table: no placement pass (k_place's
+                                      16 B of writes per record) before it; 0 places every
+                                      exchange.  Same output. */
 
 /* ---- geometry: DistributedArray::create (mpi/mpi_lsbsort.cpp:144-149) ---- */
 int64_t lsb_per_rank(int64_t n_total, int num_ranks);            /* ceil(n/P) */

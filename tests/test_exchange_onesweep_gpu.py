@@ -176,3 +176,30 @@ def test_golden_digests_loopback(lsb_built, oracle_mod, digests):
                 w.generate()
                 w.my_sort()
                 assert oracle_mod.digest(w.gather_global()) == d["output"], (d["n"], d["P"], bits)
+
+
+@pytest.mark.parametrize("n,P,bits", [(1 << 22, 2, 8), (1 << 22, 3, 16), (3 * T + 11, 2, 16),
+                                      ((1 << 21) + 5, 8, 8), (600_011, 5, 16)])
+def test_gathered_pass_matches_placed(lsb_built, oracle_mod, n, P, bits):
+    """LSB_OPT_EXCHANGE_GATHER (the default): every exchange but the last only
+    counts the next byte, and the next pass reads its tiles where the records
+    arrived (receive buffer, the rank's own segment in A) through the plan's
+    piece table.  Long pieces (8-bit digits: a few per tile, the tile
+    descriptors) and short ones (16-bit digits at these sizes: the per-record
+    search) both give the placed form's output (LSB_OPT_EXCHANGE_GATHER = 0),
+    the oracle's stable sort, and the same k_place launches (count-only or
+    placing)."""
+    a = _uniform(n, n + P)
+    outs, stats = [], []
+    for g in (1, 0):
+        with lsb_built.World(a.size, ranks=P, radix_bits=bits) as w:
+            w.set_option(lsb_built.OPT_EXCHANGE_GATHER, g)
+            w.scatter_global(a)
+            w.set_timing(True)
+            w.my_sort()
+            outs.append(w.gather_global())
+            stats.append(w.kernel_stats())
+    assert np.array_equal(outs[0], oracle_mod.stable_sort(a))
+    assert np.array_equal(outs[0], outs[1])
+    assert stats[0]["place"][0] == stats[1]["place"][0]
+    assert stats[0]["upsweep"][0] == stats[1]["upsweep"][0] == P  # one k_subhist per rank

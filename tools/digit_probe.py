@@ -20,6 +20,8 @@ if os.environ.get("LSB_SPLIT"):  # LSB_OPT_ONESWEEP_SPLIT: 0 auto, 1 never, 2 al
     w.set_option(lsbsort.OPT_ONESWEEP_SPLIT, int(os.environ["LSB_SPLIT"]))
 if os.environ.get("LSB_FORCE_EXCHANGE") == "1":
     w.set_option(lsbsort.OPT_FORCE_EXCHANGE, 1)
+if os.environ.get("LSB_GATHER"):  # LSB_OPT_EXCHANGE_GATHER: 0 places every exchange
+    w.set_option(lsbsort.OPT_EXCHANGE_GATHER, int(os.environ["LSB_GATHER"]))
 # LSB_PASSES=reduce-scan: count + scan + scatter per pass instead of single-read passes
 w.set_option(lsbsort.OPT_ONESWEEP, 0 if os.environ.get("LSB_PASSES") == "reduce-scan" else 1)
 # LSB_PASSES=hybrid: k top-byte passes + the segmented local sort (LSB_OPT_HYBRID)
