@@ -13,6 +13,7 @@
 #   profhyb   the same for bench.py --passes hybrid (gpurun_out/prof_hybrid;
 #             summarise with tools/pmc_summary.py TAG_hybrid gpurun_out/prof_hybrid ... --templates)
 #   sq        tools/sq_counters.sh: SQ counters of the sort at 2^28
+#   stress    tools/stress_mix.py for STRESS_S seconds (default 150): random sorts, 0 wrong
 # Output under gpurun_out/$TAG/.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -59,6 +60,11 @@ for s in $RUN; do
         || fail profhyb $O/profile_hybrid.log ;;
     sq)
       SQ_TAG=_$TAG bash tools/sq_counters.sh > $O/sq.log 2>&1 || fail sq $O/sq.log ;;
+    stress)
+      timeout -k 10 400 python -u tools/stress_mix.py --seconds ${STRESS_S:-150} --seed ${STRESS_SEED:-7} \
+        > $O/stress_mix.log 2>&1 || fail stress $O/stress_mix.log
+      tail -1 $O/stress_mix.log
+      grep -q "done: 0 of" $O/stress_mix.log || fail stress $O/stress_mix.log ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

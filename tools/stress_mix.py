@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Randomised stress of every sort form on one GPU: each iteration draws a
 size (1 .. 2^27 records, log-uniform, ragged), a rank count (P logical ranks,
-device-copy exchange), an exchange digit width (8, 16 or 64), a key
+device-copy exchange), an exchange digit width (8, 16 or 64) and whether its
+exchanges gather (LSB_OPT_EXCHANGE_GATHER), a key
 distribution, a stage form and a local-sort form (LSD or the hybrid's two
 modes), sorts, and checks lsb_verify and checkSorted.  One iteration in
 three instead sorts host-made keys (up to 2^22 records) whose bytes are
@@ -63,15 +64,17 @@ def main():
         dist = rng.choice(("uniform", "zipf"))
         split = rng.choice((0, 1, 2))
         hybrid = rng.choice((0, 1, 1, 2))
+        gather = rng.choice((0, 1, 1))  # LSB_OPT_EXCHANGE_GATHER (per-digit exchange forms)
         host = rng.random() < 1 / 3
         if host:
             n = min(n, 1 << 22)
             dist = "thinned"
-        desc = f"iter {it}: n={n} P={P} bits={bits} dist={dist} split={split} hybrid={hybrid}"
+        desc = f"iter {it}: n={n} P={P} bits={bits} dist={dist} split={split} hybrid={hybrid} gather={gather}"
         try:
             with lsbsort.World(n, ranks=P, radix_bits=bits) as w:
                 w.set_option(lsbsort.OPT_ONESWEEP_SPLIT, split)
                 w.set_option(lsbsort.OPT_HYBRID, hybrid)
+                w.set_option(lsbsort.OPT_EXCHANGE_GATHER, gather)
                 if host:
                     arr = thinned_keys(rng, n)
                     w.scatter_global(arr)
