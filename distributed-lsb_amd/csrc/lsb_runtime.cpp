@@ -1400,7 +1400,8 @@ int sort_exchange_onesweep(lsb_ctx* c) {
     if (!st.exch) continue;
     for (Rank& r : c->ranks) {
       r.place_next = c->peer || r.here == 0 ? -1 : after;
-      r.gather_next = c->gather && r.place_next >= 0;
+      // Not with the split stage (skewed keys): its gathered instances spill.
+      r.gather_next = c->gather && r.place_next >= 0 && r.os_halves == 1;
       r.place_hist = nullptr;
       if (r.place_next >= 0) {
         r.place_hist = r.os_hist + (size_t)(r.os_cur ^ 1) * lsb::kOnesweepSubs * lsb::kBuckets;
