@@ -1,0 +1,48 @@
+#!/usr/bin/env python3
+"""Does where a context's record buffers land change the pass speed?
+(development probe; DESIGN.md §4 box-to-box spread)
+
+Several contexts of 2^LG records are created one after another in one
+process, each kept alive while the next is made, and each sorts the PCG
+input REPS times; the per-pass k_onesweep times (lsb_get_pass_stats) show
+whether the first buffers allocated in a fresh process run slower than later
+ones.
+
+    python tools/alloc_probe.py [LG] [CONTEXTS] [REPS]
+"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "distributed-lsb_amd"))
+import lsbsort  # noqa: E402
+
+lg = int(sys.argv[1]) if len(sys.argv) > 1 else 30
+ctxs = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+reps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+n = 1 << lg
+worlds = []
+for c in range(ctxs):
+    w = lsbsort.World(n, ranks=1, radix_bits=8)
+    worlds.append(w)
+    w.generate()
+    w.my_sort()  # warm-up (allocates the look-back rows)
+    w.sync()
+    for r in range(reps):
+        w.generate()
+        w.sync()
+        w.reset_kernel_stats()
+        w.set_timing(True)
+        t0 = time.perf_counter()
+        w.my_sort()
+        w.sync()
+        ms = (time.perf_counter() - t0) * 1e3
+        passes = [round(p["ms_scatter"], 3) for p in w.pass_stats()]
+        w.set_timing(False)
+        print(json.dumps({"context": c, "rep": r, "ms": round(ms, 2), "passes": passes}), flush=True)
+    ok, _ = w.verify()
+    print(json.dumps({"context": c, "verified": ok}), flush=True)
+for w in worlds:
+    w.close()
