@@ -9,6 +9,10 @@ whether the first buffers allocated in a fresh process run slower than later
 ones.
 
     python tools/alloc_probe.py [LG] [CONTEXTS] [REPS]
+
+(A build whose record buffers came from hipExtMallocWithFlags(...,
+hipDeviceMallocContiguous) ran every pass ~48 % slower, 10.3-10.9 ms:
+profiles/ab/r03_alloc_contig.log; not kept.)
 """
 import json
 import os
