@@ -56,6 +56,11 @@ HBM_PEAK_GBS = 8000.0           # MI355X HBM3E spec (MI355X_MICROARCH.md)
 SCATTER_BYTES_PER_ELEM = 32     # 16 B read + 16 B written per record per pass
 COUNT_BYTES_PER_ELEM = 16       # histogram read of the keys' lines
 REF_MPI_MELEMS = 830.0          # mpi_lsbsort, 64 nodes x 128 cores, n = 2^36
+XGMI_LINK_GBS = 153.0           # per xGMI link of an MI355X (spec figure, see XGMI_PEAK_SOURCE)
+XGMI_PEAK_SOURCE = ("spec figure, not measured here: MI355X, 7 xGMI links x ~153 GB/s per GPU, one direct link "
+                    "per GPU pair on an 8-GPU node (task brief; SURVEY.md 5 and 8(d), which prices the per-pass "
+                    "exchange as 16*m/P bytes per link at 153 GB/s); frac = the busiest link's bytes in one "
+                    "direction / its sender's wire time / 153 GB/s")
 
 
 def parse():
@@ -72,10 +77,13 @@ def parse():
                     help="skip the rocprofv3 --pmc passes that measure the dominant kernel's HBM bytes")
     ap.add_argument("--no-whole-key", action="store_true",
                     help="N > 1: skip the extra whole-key exchange timing")
+    ap.add_argument("--no-peer", action="store_true",
+                    help="N > 1: skip the extra peer-store exchange timing (LSB_OPT_EXCHANGE_PEER)")
     ap.add_argument("--probe", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--dry-rank", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--dry-fail", type=int, default=-1, help=argparse.SUPPRESS)
     ap.add_argument("--dry-fail-whole-key", type=int, default=-1, help=argparse.SUPPRESS)
+    ap.add_argument("--dry-fail-peer", type=int, default=-1, help=argparse.SUPPRESS)
     ap.add_argument("--rank-timeout", type=int, default=1500,
                     help="self-launched rank processes: seconds before they are stopped")
     ap.add_argument("--no-verify", action="store_true")
@@ -137,6 +145,14 @@ class Dist:
         t = torch.tensor(list(xs), dtype=torch.float64)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return [float(v) for v in t.tolist()]
+
+    def all_gather_obj(self, obj):
+        """[obj of rank 0, obj of rank 1, ...] on every rank."""
+        if not self.dist:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
 
     def all_true(self, ok):
         if not self.dist:
@@ -527,6 +543,31 @@ def whole_key_argv(a):
                       (["--passes", "hybrid"] if a.passes == "onesweep" else []))
 
 
+def peer_argv(a):
+    """The peer-store extra: the headline's per-digit exchange with direct
+    stores into the owners' buffers (LSB_OPT_EXCHANGE_PEER; the reference's
+    shmem_putmem / MPI_Put form, shmem/shmem_lsbsort.cpp:441-456,
+    mpi/mpi_lsbsort_onesided.cpp:487-509), verified by lsb_verify."""
+    return extra_argv(a, ["--exchange", "peer", "--radix-bits", str(a.radix_bits or 16)])
+
+
+def extras_at(a, N):
+    """The extra forms timed after the headline, in fresh processes: (name,
+    argv).  N > 1: the whole-key exchange and the peer-store exchange (unless
+    the headline already is that form); N = 1: the hybrid local sort."""
+    if a.no_extras:
+        return []
+    radix = a.radix_bits or (8 if N == 1 else 16)
+    if N == 1:
+        return [("hybrid", extra_argv(a, ["--passes", "hybrid"]))] if a.passes == "onesweep" else []
+    out = []
+    if radix != 64 and not a.no_whole_key:
+        out.append(("whole_key", whole_key_argv(a)))
+    if radix != 64 and a.exchange != "peer" and not a.no_peer and a.transport != "gloo":
+        out.append(("peer", peer_argv(a)))
+    return out
+
+
 def merge_extra(out, name, ok, text, report):
     """An extra form's keys into the headline line: <name>_melem_s,
     _ms_per_step, _verified (and its per-pass rows and dominant-kernel
@@ -538,44 +579,56 @@ def merge_extra(out, name, ok, text, report):
     out[f"{name}_melem_s"] = r["value"]
     out[f"{name}_ms_per_step"] = r["ms_per_step"]
     out[f"{name}_verified"] = r["verified"]
-    for k in ("per_pass", "kernel_ms_per_step", "roofline"):
+    for k in ("per_pass", "kernel_ms_per_step", "roofline", "exchange_roofline"):
         if r.get(k) is not None:
             out[f"{name}_{k}"] = r[k]
 
 
-def merge_whole_key(out, ok, text, report):
-    merge_extra(out, "whole_key", ok, text, report)
-
-
-def rank_whole_key(a, d, out):
-    """Launcher-started ranks (torch.distributed.run): the whole-key exchange
-    (one all-to-all per sort), same input, fewer steps, in one fresh process
-    per rank (this rank's context is closed by now), so a failure there costs
-    only its own keys.  Every rank takes the same branch: the children's
-    success is agreed on before rank 0 reads its child's line."""
+def rank_extra(a, d, out, name, argv):
+    """Launcher-started ranks (torch.distributed.run): an extra form, same
+    input, fewer steps, in one fresh process per rank (this rank's context is
+    closed by now), so a failure there costs only its own keys.  Every rank
+    takes the same branch: the children's success is agreed on before rank 0
+    reads its child's line."""
     port = d.bcast_bytes(free_port() if d.rank == 0 else None)
     env = rank_env(d.rank, d.world, d.local_rank, port, os.environ.get("MASTER_ADDR", "127.0.0.1"))
-    ok, text, report = spawn_ranks(whole_key_argv(a), [env], a.rank_timeout, "whole-key extra")
+    ok, text, report = spawn_ranks(argv, [env], a.rank_timeout, f"{name} extra")
     ok = d.all_true(ok)
     if d.rank == 0:
-        merge_whole_key(out, ok, text, report or ("" if ok else "another rank's process failed"))
+        merge_extra(out, name, ok, text, report or ("" if ok else "another rank's process failed"))
+
+
+def dry_stats(rank, P, steps):
+    """Exchange stats of the shape lsb_get_exchange_stats reports, made up
+    for --dry-rank (rank r sends (r + 1) MB to every peer per exchange)."""
+    per = [0 if q == rank else (rank + 1) << 20 for q in range(P)]
+    ex = 4 * steps
+    return {"exchanges": ex, "calls": 4 * ex, "sent_bytes": [b * ex for b in per],
+            "recv_bytes": [0 if q == rank else ((q + 1) << 20) * ex for q in range(P)],
+            "wire_ms": 1.0 * ex, "plan_ms": 0.1 * ex, "place_ms": 0.5 * ex, "place_tail_ms": 0.125 * ex,
+            "place_bytes": 32 * 1000 * ex, "placed_records": 1000 * steps, "counted_records": 3000 * steps}
 
 
 def dry_run(a):
     """--dry-rank (tests, CPU): the launch plumbing without a GPU.  Each rank
     joins the gloo group and max-reduces its rank; rank 0 prints a line of
-    the bench's shape; --dry-fail R makes rank R exit with status 3 (and
-    --dry-fail-whole-key R rank R of the whole-key extra)."""
+    the bench's shape (with an exchange roofline from made-up stats at
+    N > 1); --dry-fail R makes rank R exit with status 3 (and
+    --dry-fail-whole-key / --dry-fail-peer R rank R of that extra)."""
     d = Dist()
     radix = a.radix_bits or (8 if d.world == 1 else 16)
-    if d.rank == (a.dry_fail_whole_key if radix == 64 else a.dry_fail):
+    fail = a.dry_fail_whole_key if radix == 64 else a.dry_fail_peer if a.exchange == "peer" else a.dry_fail
+    if d.rank == fail:
         sys.exit(3)
     top = d.max(float(d.rank))
     out = {"metric": METRIC, "value": float(d.world * radix), "ms_per_step": 1.0, "verified": True,
-           "n_gpus": d.world, "max_rank": top, "radix_bits": radix,
+           "n_gpus": d.world, "max_rank": top, "radix_bits": radix, "exchange": a.exchange,
            "config": {"n_total": a.n_per_gpu * d.world}}
-    if d.world > 1 and radix != 64 and not (a.no_whole_key or a.no_extras):
-        rank_whole_key(a, d, out)
+    if d.world > 1:
+        out["exchange_roofline"] = exchange_roofline(
+            d.all_gather_obj({"stats": dry_stats(d.rank, d.world, a.steps)}), a.steps)
+        for name, argv in extras_at(a, d.world):
+            rank_extra(a, d, out, name, argv)
     d.barrier()
     d.close()
     if d.rank == 0:
@@ -597,11 +650,10 @@ def launch(a):
         print(f"bench.py: {report or 'rank 0 printed no result line'}", file=sys.stderr, flush=True)
         sys.exit(1)
     out["launcher"] = f"bench.py started {N} rank processes (one per GPU)"
-    radix = a.radix_bits or 16
-    if radix != 64 and not (a.no_whole_key or a.no_extras):
+    for name, xargv in extras_at(a, N):
         port = free_port()
-        merge_whole_key(out, *spawn_ranks(whole_key_argv(a), [rank_env(r, N, r, port) for r in range(N)],
-                                          a.rank_timeout, "whole-key extra"))
+        merge_extra(out, name, *spawn_ranks(xargv, [rank_env(r, N, r, port) for r in range(N)],
+                                            a.rank_timeout, f"{name} extra"))
     out["cpu_baseline"] = None if a.no_cpu_baseline else cpu_baseline(out["config"]["n_total"], a.cpu_n)
     print(json.dumps(out), flush=True)
     if out.get("verified") is False or out.get("whole_key_verified") is False:
@@ -620,10 +672,66 @@ def probe(a):
     w.close()
 
 
+def exchange_roofline(ranks, steps):
+    """The exchange side of a sort at N > 1 ("the k_place
+    bytes" and "the xGMI bound: each GPU sends 16*m/P B to each of its P-1
+    peers per pass"), from every rank's lsb_get_exchange_stats (`ranks[r]
+    ["stats"]`, summed over `steps` sorts).  Per sort: the payload each rank
+    handed RCCL and per directed link (busiest / least busy pair: the skew of
+    Zipf keys shows here), the all-to-all's wire time on the ranks' streams
+    (plan and placement excluded), the busiest link's achieved GB/s and its
+    fraction of the per-link xGMI figure, each GPU's send rate, and the
+    placement (k_place / merge) bytes, time and the part of it left after the
+    last slice arrived (not overlapped with the wire)."""
+    P = len(ranks)
+    st = [r["stats"] for r in ranks]
+    S = [[st[s]["sent_bytes"][q] / steps for q in range(P)] for s in range(P)]
+    links = sorted((S[s][q], s, q) for s in range(P) for q in range(P) if q != s)
+    wire = [x["wire_ms"] / steps for x in st]
+    ex = st[0]["exchanges"] / steps
+
+    def gbs(b, ms):
+        return round(b / (ms / 1e3) / 1e9, 2) if ms > 0 else None
+
+    hi, lo = links[-1], links[0]
+    link_gbs = gbs(hi[0], wire[hi[1]])
+    sent = [sum(S[s][q] for q in range(P) if q != s) for s in range(P)]
+    gpu = [g for g in (gbs(sent[s], wire[s]) for s in range(P)) if g is not None]
+    place_ms = [x["place_ms"] / steps for x in st]
+    tail = [x["place_tail_ms"] / steps for x in st]
+    pbytes = [x["place_bytes"] / steps for x in st]
+    busy = max(range(P), key=lambda r: place_ms[r])
+    return {
+        "bound": "xgmi", "unit": "GB/s", "peak": XGMI_LINK_GBS, "peak_source": XGMI_PEAK_SOURCE,
+        "achieved": link_gbs, "frac": round(link_gbs / XGMI_LINK_GBS, 4) if link_gbs else None,
+        "exchanges_per_sort": ex, "calls_per_sort": st[0]["calls"] / steps,
+        "rank_bytes_per_sort": {"max": int(max(sent)), "min": int(min(sent))},
+        "link_bytes_per_sort": {"max": int(hi[0]), "max_link": [hi[1], hi[2]],
+                                "min": int(lo[0]), "min_link": [lo[1], lo[2]],
+                                "max_over_min": round(hi[0] / lo[0], 3) if lo[0] else None},
+        "link_bytes_per_exchange": {"max": int(hi[0] / ex) if ex else None,
+                                    "min": int(lo[0] / ex) if ex else None},
+        "wire_ms_per_sort": {"max": round(max(wire), 3), "min": round(min(wire), 3)},
+        "gpu_send_gbs": {"max": max(gpu), "min": min(gpu)} if gpu else None,
+        "link_bound_ms_per_sort": round(hi[0] / (XGMI_LINK_GBS * 1e9) * 1e3, 3),
+        "plan_ms_per_sort": round(max(x["plan_ms"] / steps for x in st), 3),
+        "place": {"bytes_per_sort": int(pbytes[busy]), "ms_per_sort": round(place_ms[busy], 3),
+                  "gbs": gbs(pbytes[busy], place_ms[busy]), "tail_ms_per_sort": round(max(tail), 3),
+                  "overlapped_frac": round(min(1 - t / m for t, m in zip(tail, place_ms) if m > 0), 4)
+                  if any(m > 0 for m in place_ms) else None,
+                  "placed_records_per_sort": int(st[busy]["placed_records"] / steps),
+                  "counted_records_per_sort": int(st[busy]["counted_records"] / steps),
+                  "basis": "rank with the longest placement; 32 B per placed record, 16 B per "
+                           "counted one, 32 B per merge level"},
+    }
+
+
 def per_pass_rows(passes, steps, kernel, N):
     """Per local pass, per step (lsb_get_pass_stats): the scatter kernel's
     time, its HBM rate (32 algorithmic bytes per record) and its fraction of
-    the peak, plus the pass's count, exchange and placement time."""
+    the peak, plus the pass's count, exchange and placement time; with an
+    exchange after the pass, its all-to-all payload, wire time and rate
+    (this rank's) and the placement tail."""
     rows = []
     for p in passes:
         if not p["launches"]:
@@ -638,6 +746,11 @@ def per_pass_rows(passes, steps, kernel, N):
         if N > 1 or p["ms_exchange"] or p["ms_place"]:
             row["exchange_ms"] = round(p["ms_exchange"] / steps, 4)
             row["place_ms"] = round(p["ms_place"] / steps, 4)
+        if p.get("ms_wire"):
+            row["exchange_bytes"] = int(p["exchange_bytes"] / steps)
+            row["wire_ms"] = round(p["ms_wire"] / steps, 4)
+            row["exchange_gbs"] = round(p["exchange_bytes"] / (p["ms_wire"] / 1e3) / 1e9, 2)
+            row["place_tail_ms"] = round(p["ms_place_tail"] / steps, 4)
         rows.append(row)
     return rows
 
@@ -668,8 +781,10 @@ def main():
     passes = w.pass_stats()
     scatter_elems = w.scatter_elems()
     xcalls, xbytes, _ = w.exchange_bytes()
+    xstats = w.exchange_stats()
     last = w.last_sort()
     w.close()
+    xroof = exchange_roofline(d.all_gather_obj({"stats": xstats}), a.steps) if N > 1 else None
 
     ms_per_step = total / a.steps * 1e3
     value = n_total * a.steps / total / 1e6
@@ -766,18 +881,18 @@ def main():
             "place": "placement stream: merge of the received runs (whole key) or k_place",
             "sort": "the whole sort, per rank"},
         "exchange_bytes_per_step": xbytes // a.steps if N > 1 else 0,
+        "exchange_roofline": xroof,
         "verified": verified,
         "vs_baseline_basis": "MPI mpi_lsbsort 830 M elem/s (64 nodes x 128 cores, n=2^36; BASELINE.md §1)",
         "library": lsbsort.build_info(),
     }
-    if N > 1 and radix != 64 and not (a.no_whole_key or a.no_extras):
-        rank_whole_key(a, d, out)
-    if N == 1 and a.passes == "onesweep" and not a.no_extras:
-        # The hybrid local sort (same output, fewer passes over HBM), in a
-        # fresh process of its own, after the headline.
-        ok, text, report = spawn_ranks(extra_argv(a, ["--passes", "hybrid"]), [dict(os.environ)],
-                                       a.rank_timeout, "hybrid extra")
-        merge_extra(out, "hybrid", ok, text, report)
+    # The extra forms, in fresh processes after the headline: N > 1 the
+    # whole-key and peer-store exchanges, N = 1 the hybrid local sort.
+    for name, xargv in extras_at(a, N):
+        if N > 1:
+            rank_extra(a, d, out, name, xargv)
+        else:
+            merge_extra(out, name, *spawn_ranks(xargv, [dict(os.environ)], a.rank_timeout, f"{name} extra"))
     if d.rank == 0 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(n_total, a.cpu_n)
     elif d.rank == 0:

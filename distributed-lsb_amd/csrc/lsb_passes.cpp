@@ -1,0 +1,476 @@
+// The local pass driver (mySort's localShuffle, mpi/mpi_lsbsort.cpp:213-247,
+// and the pass loop of :580-585 when nothing is exchanged):
+//   * reduce-then-scan passes (k_upsweep + k_scan + k_scatter; lsb_pass and
+//     LSB_OPT_ONESWEEP = 0), and the digit loop do_pass that follows each
+//     exchange digit's local passes with its exchange (lsb_exchange.cpp);
+//   * single-read passes: one k_subhist read per sort, then one k_onesweep
+//     per varying byte (decoupled look-back), histograms carried from pass to
+//     pass;
+//   * the hybrid local sort (LSB_OPT_HYBRID): k_onesweep on the top varying
+//     bytes, segments ordered by k_segfix / k_segsort (lsb_segsort.hip).
+#include "lsb_rt.h"
+
+namespace lsb_rt {
+
+// ---- one local stable 8-bit pass A -> B, then swap (localShuffle) -------
+// want_span: also reduce the key span (lsb_sort's first pass).  starts16:
+// this is the high byte of a 16-bit exchange digit; the scatter also marks
+// the digit's run starts, so digit_counts needs no extra read.
+int local_pass(lsb_ctx* c, Rank& r, int shift, bool want_span, bool starts16) {
+  HIP_TRY(hipSetDevice(r.dev));
+  r.starts_fused = starts16;
+  if (r.here == 0) {
+    HIP_TRY(hipMemsetAsync(r.totals, 0, sizeof(uint64_t) * lsb::kBuckets, r.stream));
+    return LSB_OK;
+  }
+  if (starts16) HIP_TRY(lsb::launch_starts_reset(r.first16, r.stream));
+  const lsb::Chunking& ch = r.chunking;
+  {
+    Timer t(c, &r, LSB_K_UPSWEEP);
+    HIP_TRY(lsb::launch_upsweep(r.A, r.here, shift, ch, r.chunk_hist,
+                                want_span ? r.span : nullptr, r.stream));
+  }
+  {
+    Timer t(c, &r, LSB_K_SCAN);
+    HIP_TRY(lsb::launch_scan(r.chunk_hist, ch.num_chunks, r.chunk_off, r.totals, r.stream));
+  }
+  {
+    Timer t(c, &r, LSB_K_SCATTER);
+    HIP_TRY(lsb::launch_scatter(r.A, r.B, r.here, shift, ch, r.chunk_off, r.totals,
+                                starts16 ? r.first16 : nullptr, r.stream));
+    count_pass_elems(c, r.here);
+  }
+  std::swap(r.A, r.B);
+  return LSB_OK;
+}
+
+// One exchange digit: its 8-bit local sub-passes, then (P > 1) the exchange.
+// varying: key bits that differ somewhere; a sub-pass whose byte is constant
+// is the identity and is skipped (all ~0 = run everything).  want_span: the
+// first sub-pass also reduces the key span (lsb_sort, digit 0).
+
+int do_pass(lsb_ctx* c, int digit, uint64_t varying, bool want_span) {
+  if (c->bits == 64 && exchanging(c)) return merge_sort(c);  // the one 64-bit digit
+  for (Rank& r : c->ranks) r.starts_fused = false;
+  const int subs = c->bits / lsb::kDigitBits;
+  for (int sub = 0; sub < subs; ++sub) {
+    const int shift = digit * c->bits + sub * lsb::kDigitBits;
+    if (!want_span && ((varying >> shift) & (lsb::kBuckets - 1)) == 0) continue;
+    // The high byte of a 16-bit exchange digit also marks the digit's starts.
+    const bool starts16 = exchanging(c) && subs == 2 && sub == 1;
+    begin_pass(c, shift);
+    for (Rank& r : c->ranks) LSB_TRY(local_pass(c, r, shift, want_span && sub == 0, starts16));
+    ++c->last_local_passes;
+  }
+  if (!exchanging(c)) return LSB_OK;
+  ++c->last_exchanges;
+  return exchange_digit(c, digit);
+}
+
+// ---- single-read passes (P == 1) ------------------------------------------
+bool onesweep_applies(const lsb_ctx* c) {
+  return c->onesweep && !exchanging(c) && c->ranks.size() == 1 && c->ranks[0].here > 0 &&
+         c->ranks[0].here <= lsb::kOnesweepMaxElems;
+}
+
+int onesweep_ensure(Rank& r) {
+  if (r.os_status) return LSB_OK;
+  const size_t tiles = (size_t)lsb::onesweep_tiles(r.here);
+  LSB_TRY(dev_alloc(&r.os_status, tiles * lsb::kBuckets));
+  LSB_TRY(dev_alloc(&r.os_hist, 2 * lsb::kOnesweepSubs * lsb::kBuckets));
+  LSB_TRY(dev_alloc(&r.os_ctr, 2 * lsb::kOnesweepSubs));
+  LSB_TRY(host_alloc(&r.os_err_h, 2));  // [0] look-back gave up, [1] k_segsort error
+  r.os_err_h[0] = r.os_err_h[1] = 0;
+  LSB_TRY(host_alloc(&r.os_hist_h, (size_t)lsb::kOnesweepSubs * lsb::kBuckets));
+  HIP_TRY(hipMemsetAsync(r.os_status, 0, tiles * lsb::kBuckets * sizeof(uint32_t), r.stream));
+  HIP_TRY(hipMemsetAsync(r.os_ctr, 0, 2 * lsb::kOnesweepSubs * sizeof(uint32_t), r.stream));
+  r.os_epoch = 0;
+  r.os_grid = max_chunks_for_device(r.dev);
+  return LSB_OK;
+}
+
+// One k_onesweep launch of rank r, r.A -> r.B on the byte at `shift` (then
+// the buffers swap), under a fresh look-back epoch.  Granules carry the
+// epoch's parity, and every launch rewrites every row, so only the
+// alternation matters (the counter runs on for the record).  The epoch
+// advances only once the launch is queued: a launch that fails before its
+// kernel runs writes no rows, and a later launch would then accept rows of
+// two launches back as current.  So a failure marks the rows dirty; the next
+// launch zeroes them first and restarts the epochs (the first is odd).
+int onesweep_launch(lsb_ctx* c, Rank& r, int shift, int next, const uint32_t* hist,
+                    uint32_t* next_hist, lsb::OnesweepExtra x) {
+  const size_t status_bytes = (size_t)lsb::onesweep_tiles(r.here) * lsb::kBuckets * sizeof(uint32_t);
+  if (r.os_dirty) {
+    HIP_TRY(hipMemsetAsync(r.os_status, 0, status_bytes, r.stream));
+    r.os_epoch = 0;
+    r.os_dirty = false;
+  }
+  uint32_t epoch = r.os_epoch + 1;
+  if (epoch >= (1u << 30)) epoch = 2;  // 2^30 is even: keep the alternation
+  hipError_t e;
+  if (c->fail_onesweep > 0 && --c->fail_onesweep == 0) {  // LSB_OPT_FAIL_ONESWEEP (tests)
+    r.os_dirty = true;
+    return fail(LSB_ERR_HIP, "launch_onesweep", "injected launch failure (LSB_OPT_FAIL_ONESWEEP)");
+  }
+  {
+    Timer t(c, &r, LSB_K_SCATTER);
+    e = lsb::launch_onesweep(r.A, r.B, r.here, shift, next, hist, next_hist, r.os_status, r.os_ctr,
+                             epoch, r.os_ctr + lsb::kOnesweepSubs, r.os_grid, r.stream, x);
+  }
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    r.os_dirty = true;
+    return fail(LSB_ERR_HIP, "launch_onesweep", hipGetErrorString(e));
+  }
+  r.os_epoch = epoch;
+  count_pass_elems(c, r.here);
+  std::swap(r.A, r.B);
+  return LSB_OK;
+}
+
+// This sort's k_onesweep stage split for rank r (LSB_OPT_ONESWEEP_SPLIT).
+// Auto decides from the first digit's sub-array histogram (`hist`, on
+// r.stream): queue_halves queues its 8 KiB read-back, to share the span's
+// stream sync; choose_halves decides after that sync.
+int queue_halves(lsb_ctx* c, Rank& r, const uint32_t* hist) {
+  if (c->os_split != 0 || r.here == 0) return LSB_OK;
+  HIP_TRY(hipMemcpyAsync(r.os_hist_h, hist, sizeof(uint32_t) * lsb::kOnesweepSubs * lsb::kBuckets,
+                         hipMemcpyDeviceToHost, r.stream));
+  return LSB_OK;
+}
+
+int choose_halves(lsb_ctx* c, Rank& r, bool synced) {
+  if (c->os_split != 0 || r.here == 0) {
+    r.os_halves = c->os_split == 2 ? 2 : 1;
+    return LSB_OK;
+  }
+  if (!synced) HIP_TRY(hipStreamSynchronize(r.stream));
+  r.os_halves = lsb::onesweep_halves_for(r.os_hist_h, r.here);
+  return LSB_OK;
+}
+
+// k_subhist of the byte `byte` of rank r's A into os_hist[0] (the sub-array
+// histogram the first pass reads), with the key span when `span`.
+int count_byte(lsb_ctx* c, Rank& r, int byte, bool span) {
+  Timer t(c, &r, LSB_K_UPSWEEP);
+  HIP_TRY(lsb::launch_subhist(r.A, r.here, byte * lsb::kDigitBits, r.os_grid, r.os_hist,
+                              span ? r.span : nullptr, r.stream));
+  return LSB_OK;
+}
+
+// The bytes of `varying` (ascending): the digits a sort must run.
+std::vector<int> varying_bytes(uint64_t varying) {
+  std::vector<int> d;
+  for (int b = 0; b < 64 / lsb::kDigitBits; ++b)
+    if (((varying >> (b * lsb::kDigitBits)) & (lsb::kBuckets - 1)) != 0) d.push_back(b);
+  return d;
+}
+
+// One k_onesweep pass per byte of `digits` (ascending), r.A -> r.B ->
+// ..., each also counting the next byte over its output; os_hist[0] holds
+// the sub-array histogram of digits[0] over r.A.
+int onesweep_digits(lsb_ctx* c, Rank& r, const std::vector<int>& digits, int* passes) {
+  uint32_t* hist[2] = {r.os_hist, r.os_hist + lsb::kOnesweepSubs * lsb::kBuckets};
+  for (size_t i = 0; i < digits.size(); ++i) {
+    const int shift = digits[i] * lsb::kDigitBits;
+    const int next = i + 1 < digits.size() ? digits[i + 1] * lsb::kDigitBits : -1;
+    begin_pass(c, shift);
+    lsb::OnesweepExtra x;
+    x.halves = r.os_halves;
+    LSB_TRY(onesweep_launch(c, r, shift, next, hist[i & 1], hist[(i + 1) & 1], x));
+    ++*passes;
+  }
+  return LSB_OK;
+}
+
+int sort_hybrid_rank(lsb_ctx* c, Rank& r, int* passes, uint64_t* varying);
+
+// lsb_sort when nothing is exchanged: one k_subhist read (digit 0's
+// sub-array histogram and the key span), then one k_onesweep per digit that
+// varies, each also counting the next such digit over its output.  Same
+// output as the reduce-then-scan loop (do_pass).  A constant digit 0 is
+// skipped like any other: its pass would be the identity, so the first
+// digit that varies is counted by a second k_subhist read (a read, not a
+// pass), and that digit's histogram also decides the stage split.
+// Rank r alone (its local block); *passes gets the passes it ran, *varying the
+// key bits that vary in the block.  LSB_OPT_HYBRID: sort_hybrid_rank.
+int sort_onesweep_rank(lsb_ctx* c, Rank& r, int* passes, uint64_t* varying) {
+  if (c->hybrid) return sort_hybrid_rank(c, r, passes, varying);
+  HIP_TRY(hipSetDevice(r.dev));
+  LSB_TRY(onesweep_ensure(r));
+  c->pass_cursor = 0;
+  c->cur_pass = 0;  // the count reads are filed under the first pass
+  HIP_TRY(hipMemsetAsync(r.span, 0, 2 * sizeof(uint64_t), r.stream));
+  LSB_TRY(count_byte(c, r, 0, c->skip_constant));
+  LSB_TRY(queue_halves(c, r, r.os_hist));
+  *varying = ~0ull;
+  *passes = 0;
+  if (c->skip_constant) {
+    HIP_TRY(hipMemcpyAsync(r.span_h, r.span, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, r.stream));
+    HIP_TRY(hipStreamSynchronize(r.stream));
+    *varying = r.span_h[0] & r.span_h[1];
+  }
+  const std::vector<int> digits = varying_bytes(*varying);
+  if (!digits.empty() && digits[0] != 0) {
+    LSB_TRY(count_byte(c, r, digits[0], false));
+    LSB_TRY(queue_halves(c, r, r.os_hist));
+    LSB_TRY(choose_halves(c, r, false));
+  } else {
+    LSB_TRY(choose_halves(c, r, c->skip_constant));
+  }
+  LSB_TRY(onesweep_digits(c, r, digits, passes));
+  // The look-back's give-up word, read by lsb_sync.
+  HIP_TRY(hipMemcpyAsync(r.os_err_h, r.os_ctr + lsb::kOnesweepSubs, sizeof(uint32_t),
+                         hipMemcpyDeviceToHost, r.stream));
+  return LSB_OK;
+}
+
+// ---- hybrid local sort (LSB_OPT_HYBRID) ------------------------------------
+// The same stable order as the LSD passes from fewer passes over HBM
+// (lsb_segsort.hip): k_onesweep passes on the k most significant varying
+// bytes only, then k_segsort orders every segment (run of records equal on
+// those bytes) by the whole key.  k: the fewest top varying bytes whose
+// varying bits reach ceil(log2 m), so uniform keys leave segments of about
+// one record (2^30 records: k = 4, 0.25 on average; k_segsort's walk then
+// costs ~2 LDS reads per record and the pass streams at copy speed.  k = 3,
+// 64 per segment, made k_segsort compute-bound: 69 ms against 7 for the
+// fourth byte's pass, profiles/r03_h1_probe.log).
+std::vector<int> hybrid_bytes(uint64_t varying, int64_t m) {
+  int need = 0;
+  while ((int64_t(1) << need) < m) ++need;
+  std::vector<int> top;
+  int bits = 0;
+  for (int b = 64 / lsb::kDigitBits - 1; b >= 0 && bits < need; --b) {
+    const uint64_t v = (varying >> (b * lsb::kDigitBits)) & (lsb::kBuckets - 1);
+    if (!v) continue;
+    top.insert(top.begin(), b);
+    bits += __builtin_popcountll(v);
+  }
+  return top;
+}
+
+// The hybrid for rank r.  The k passes leave the input A untouched (A -> B,
+// then B <-> R), so when k_segsort meets a segment longer than kSegMax the
+// sort starts over from A with the LSD passes; skewed keys (the first
+// pass's byte has a bucket over 1/32 of the records, as for the stage
+// split: duplicate-heavy keys make long segments) take them directly.  One
+// host sync, after k_segsort, reads its error word.
+int sort_hybrid_rank(lsb_ctx* c, Rank& r, int* passes, uint64_t* varying) {
+  HIP_TRY(hipSetDevice(r.dev));
+  LSB_TRY(onesweep_ensure(r));
+  LSB_TRY(ensure_recv(c, r));
+  c->pass_cursor = 0;
+  c->cur_pass = 0;
+  const int64_t m = r.here;
+  *passes = 0;
+  *varying = ~0ull;
+  // Count the byte the first pass most likely sorts on (full 64-bit keys)
+  // in the same read as the span.
+  const std::vector<int> guess = hybrid_bytes(~0ull, m);
+  int counted = guess.empty() ? 0 : guess[0];
+  HIP_TRY(hipMemsetAsync(r.span, 0, 2 * sizeof(uint64_t), r.stream));
+  LSB_TRY(count_byte(c, r, counted, c->skip_constant));
+  if (c->skip_constant) {
+    HIP_TRY(hipMemcpyAsync(r.span_h, r.span, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, r.stream));
+    HIP_TRY(hipStreamSynchronize(r.stream));
+    *varying = r.span_h[0] & r.span_h[1];
+  }
+  const std::vector<int> digits = varying_bytes(*varying);
+  const std::vector<int> msd = c->skip_constant ? hybrid_bytes(*varying, m) : guess;
+  bool hybrid = msd.size() < digits.size();
+  // The first byte sorted on decides the stage split and whether keys are
+  // skewed (*skewed: a bucket over 1/32 of the records).
+  auto first_hist = [&](int byte, bool* skewed) -> int {
+    if (byte != counted) {
+      LSB_TRY(count_byte(c, r, byte, false));
+      counted = byte;
+    }
+    HIP_TRY(hipMemcpyAsync(r.os_hist_h, r.os_hist, sizeof(uint32_t) * lsb::kOnesweepSubs * lsb::kBuckets,
+                           hipMemcpyDeviceToHost, r.stream));
+    HIP_TRY(hipStreamSynchronize(r.stream));
+    const int h = lsb::onesweep_halves_for(r.os_hist_h, m);
+    r.os_halves = c->os_split == 0 ? h : (c->os_split == 2 ? 2 : 1);
+    *skewed = h == 2;
+    return LSB_OK;
+  };
+  bool skewed = false;
+  if (hybrid && !msd.empty()) {
+    LSB_TRY(first_hist(msd[0], &skewed));
+    if (skewed) hybrid = false;
+  }
+  if (!hybrid) {
+    if (!digits.empty()) LSB_TRY(first_hist(digits[0], &skewed));
+    LSB_TRY(onesweep_digits(c, r, digits, passes));
+  } else {
+    // The k passes: A -> B, then B <-> R; the input X0 is kept.  The last
+    // one also orders every segment inside its tile (SegPass) and k_segfix
+    // merges the segments split between tiles; LSB_OPT_HYBRID = 2, or the
+    // split stage, leaves the segments to a k_segsort pass instead.
+    Elem* const X0 = r.A;
+    Elem* const X1 = r.B;
+    Elem* const X2 = r.R;
+    // {A, B, R} stays a permutation of {X0, X1, X2} at every step (the pass
+    // loop swaps A and B; R holds X0, the kept input, from the first pass on).
+    // A return on an error restores A = X0, B = X1, R = X2, so the context
+    // keeps its input in A and three distinct buffers (advisor r03).
+    struct Restore {
+      Rank& r;
+      Elem *x0, *x1, *x2;
+      bool armed = true;
+      ~Restore() {
+        if (armed) {
+          r.A = x0;
+          r.B = x1;
+          r.R = x2;
+        }
+      }
+    } restore{r, X0, X1, X2};
+    uint64_t pmask = 0;
+    for (int b : msd) pmask |= (uint64_t)(lsb::kBuckets - 1) << (b * lsb::kDigitBits);
+    uint32_t* err = r.os_ctr + lsb::kOnesweepSubs + 1;
+    const bool fuse = c->hybrid == 1 && r.os_halves == 1 && !msd.empty();
+    lsb::SegPass sp;
+    if (fuse) {
+      if (!r.seg_base) LSB_TRY(dev_alloc(&r.seg_base, (size_t)lsb::kOnesweepSubs * lsb::kBuckets));
+      sp.pmask = pmask;
+      sp.rmask = pmask & ~((uint64_t)(lsb::kBuckets - 1) << (msd.back() * lsb::kDigitBits));
+      sp.base = r.seg_base;
+      sp.err = err;
+    }
+    HIP_TRY(hipMemsetAsync(err, 0, sizeof(uint32_t), r.stream));
+    uint32_t* hist[2] = {r.os_hist, r.os_hist + lsb::kOnesweepSubs * lsb::kBuckets};
+    const Elem* seg_in = nullptr;  // the last pass's input, read by k_segfix
+    for (size_t i = 0; i < msd.size(); ++i) {
+      const int shift = msd[i] * lsb::kDigitBits;
+      const int next = i + 1 < msd.size() ? msd[i + 1] * lsb::kDigitBits : -1;
+      begin_pass(c, shift);
+      lsb::OnesweepExtra x;
+      x.halves = r.os_halves;
+      if (fuse && i + 1 == msd.size()) {
+        x.seg = &sp;
+        seg_in = r.A;
+      }
+      LSB_TRY(onesweep_launch(c, r, shift, next, hist[i & 1], hist[(i + 1) & 1], x));
+      ++*passes;
+      if (i == 0) {  // A is X1 now, B is X0: keep X0, write X2 next
+        r.B = X2;
+        r.R = X0;
+      }
+    }
+    if (msd.empty()) {
+      r.B = X1;
+      r.R = X2;
+    }
+    auto sync_err = [&](uint32_t* v) -> int {
+      HIP_TRY(hipMemcpyAsync(r.os_err_h + 1, err, sizeof(uint32_t), hipMemcpyDeviceToHost, r.stream));
+      HIP_TRY(hipStreamSynchronize(r.stream));
+      *v = r.os_err_h[1];
+      return LSB_OK;
+    };
+    bool sorted = false;
+    if (fuse) {
+      {
+        Timer t(c, &r, LSB_K_SEGSORT);
+        // one wave per tile boundary, 32 waves per CU
+        HIP_TRY(lsb::launch_segfix(seg_in, r.A, m, msd.back() * lsb::kDigitBits, r.os_status, sp,
+                                   16 * r.os_grid, r.stream));
+      }
+      uint32_t e = 0;
+      LSB_TRY(sync_err(&e));
+      sorted = e == 0;
+    }
+    if (!sorted) {
+      // k_segsort: r.A is stably sorted by pmask (the fused pass's segments
+      // too, in or out of order).
+      HIP_TRY(hipMemsetAsync(err, 0, sizeof(uint32_t), r.stream));
+      begin_pass(c, 64);
+      {
+        Timer t(c, &r, LSB_K_SEGSORT);
+        HIP_TRY(lsb::launch_segsort(r.A, r.B, m, pmask, err, 3 * r.os_grid / 2, r.stream));
+      }
+      count_pass_elems(c, m, false);
+      ++*passes;
+      uint32_t e = 0;
+      LSB_TRY(sync_err(&e));
+      if (e == 0) {
+        std::swap(r.A, r.B);
+        sorted = true;
+      }
+    }
+    if (sorted) {
+      r.R = (X0 != r.A && X0 != r.B) ? X0 : (X1 != r.A && X1 != r.B) ? X1 : X2;
+      restore.armed = false;
+    } else {  // a segment too long for the segment sorts: the LSD passes over the kept input
+      r.A = X0;
+      r.B = X1;
+      r.R = X2;
+      restore.armed = false;
+      counted = -1;
+      if (!digits.empty()) LSB_TRY(first_hist(digits[0], &skewed));
+      LSB_TRY(onesweep_digits(c, r, digits, passes));
+    }
+  }
+  // The look-back's give-up word, read by lsb_sync.
+  HIP_TRY(hipMemcpyAsync(r.os_err_h, r.os_ctr + lsb::kOnesweepSubs, sizeof(uint32_t),
+                         hipMemcpyDeviceToHost, r.stream));
+  return LSB_OK;
+}
+
+int sort_onesweep(lsb_ctx* c) {
+  return sort_onesweep_rank(c, c->ranks[0], &c->last_local_passes, &c->last_varying);
+}
+// Rank r's block sorted on the whole key: single-read passes, or count + scan
+// + scatter when they do not apply.  Digits constant over the block are skipped.
+int sort_local_rank(lsb_ctx* c, Rank& r, int* passes, uint64_t* varying) {
+  *passes = 0;
+  *varying = 0;
+  if (r.here == 0) return LSB_OK;
+  if (c->onesweep && r.here <= lsb::kOnesweepMaxElems) return sort_onesweep_rank(c, r, passes, varying);
+  HIP_TRY(hipSetDevice(r.dev));
+  HIP_TRY(hipMemsetAsync(r.span, 0, 2 * sizeof(uint64_t), r.stream));
+  c->pass_cursor = 0;
+  begin_pass(c, 0);
+  LSB_TRY(local_pass(c, r, 0, c->skip_constant));
+  *passes = 1;
+  *varying = ~0ull;
+  if (c->skip_constant) {
+    HIP_TRY(hipMemcpyAsync(r.span_h, r.span, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, r.stream));
+    HIP_TRY(hipStreamSynchronize(r.stream));
+    *varying = r.span_h[0] & r.span_h[1];
+  }
+  for (int d = 1; d < 64 / lsb::kDigitBits; ++d) {
+    if (((*varying >> (d * lsb::kDigitBits)) & (lsb::kBuckets - 1)) == 0) continue;
+    begin_pass(c, d * lsb::kDigitBits);
+    LSB_TRY(local_pass(c, r, d * lsb::kDigitBits));
+    ++*passes;
+  }
+  return LSB_OK;
+}
+
+// After a stream sync: did a look-back give up?  (Never expected: every
+// tile's predecessors belong to running workgroups.)
+#ifdef LSB_OS_PROFILE
+void os_profile_report() {
+  unsigned long long p[10];
+  if (lsb::onesweep_profile(p, true) != hipSuccess) return;
+  const double tot = (double)(p[0] + p[1] + p[2] + p[3] + p[4] + p[5] + p[6]) + 1e-9;
+  fprintf(stderr,
+          "os_profile: dequeue %.4f load %.4f rank %.4f scan %.4f stage %.4f lookback %.4f write %.4f "
+          "(ticks %.0f; rows summed per tile %.2f over %llu tiles)\n",
+          p[0] / tot, p[6] / tot, p[1] / tot, p[2] / tot, p[3] / tot, p[5] / tot, p[4] / tot, tot,
+          p[8] ? (double)p[7] / (double)p[8] : 0.0, p[8]);
+}
+#endif
+
+int onesweep_check(Rank& r) {
+  if (!r.os_err_h || *r.os_err_h == 0) return LSB_OK;
+  *r.os_err_h = 0;
+  HIP_TRY(hipMemset(r.os_ctr + lsb::kOnesweepSubs, 0, sizeof(uint32_t)));
+  // A launch that gave up may have left rows of an older parity: start the
+  // granules over (zeroed; the next launch is odd).
+  HIP_TRY(hipMemset(r.os_status, 0, (size_t)lsb::onesweep_tiles(r.here) * lsb::kBuckets * sizeof(uint32_t)));
+  r.os_epoch = 0;
+  return fail(LSB_ERR_HIP, "k_onesweep", "look-back timed out; output invalid");
+}
+
+}  // namespace lsb_rt

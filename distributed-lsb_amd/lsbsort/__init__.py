@@ -43,8 +43,9 @@ UNIQUE_ID_BYTES = 128
 LSB_OK = 0
 LSB_ERR_VERIFY = 5
 DIST_UNIFORM, DIST_ZIPF = 0, 1
-K_UPSWEEP, K_SCAN, K_SCATTER, K_EXCHANGE, K_PLACE, K_SORT, K_SEGSORT = range(7)
-KERNEL_NAMES = ("upsweep", "scan", "scatter", "exchange", "place", "sort", "segsort")
+K_UPSWEEP, K_SCAN, K_SCATTER, K_EXCHANGE, K_PLACE, K_SORT, K_SEGSORT, K_WIRE, K_PLACE_TAIL = range(9)
+KERNEL_NAMES = ("upsweep", "scan", "scatter", "exchange", "place", "sort", "segsort", "wire", "place_tail")
+MAX_RANKS = 64
 OPT_TIMING, OPT_FORCE_EXCHANGE, OPT_SKIP_CONSTANT_DIGITS, OPT_EXCHANGE_SLICES, OPT_EXCHANGE_P2P = 0, 1, 2, 3, 4
 OPT_EXCHANGE_PEER = 5
 OPT_ONESWEEP = 6
@@ -52,6 +53,7 @@ OPT_EXCHANGE_SELF = 7
 OPT_ONESWEEP_SPLIT = 8
 OPT_HYBRID = 9
 OPT_EXCHANGE_GATHER = 10
+OPT_FAIL_ONESWEEP = 11
 MAX_PASSES = 16
 
 
@@ -74,6 +76,15 @@ _ALLTOALLV = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                               ctypes.POINTER(ctypes.c_size_t))
 _ALLREDUCE_MIN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64))
 _BARRIER = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p)
+
+
+class ExchangeStats(ctypes.Structure):
+    """lsb_exchange_stats_t."""
+    _fields_ = [("exchanges", ctypes.c_int64), ("calls", ctypes.c_int64),
+                ("sent_bytes", ctypes.c_int64 * 64), ("recv_bytes", ctypes.c_int64 * 64),
+                ("wire_ms", ctypes.c_double), ("plan_ms", ctypes.c_double), ("place_ms", ctypes.c_double),
+                ("place_tail_ms", ctypes.c_double), ("place_bytes", ctypes.c_int64),
+                ("placed_records", ctypes.c_int64), ("counted_records", ctypes.c_int64)]
 
 
 class CommOps(ctypes.Structure):
@@ -138,6 +149,7 @@ def _lib() -> ctypes.CDLL:
             "lsb_here": (i64, [i64, i32, i32]),
             "lsb_create": (i32, [ctypes.POINTER(vp), i64, i32, ctypes.POINTER(ctypes.c_int), i32]),
             "lsb_get_unique_id": (i32, [ctypes.c_char_p]),
+            "lsb_device_count": (i32, [ctypes.POINTER(ctypes.c_int)]),
             "lsb_create_rank": (i32, [ctypes.POINTER(vp), i64, i32, i32, i32, i32, ctypes.c_char_p]),
             "lsb_create_rank_ops": (i32, [ctypes.POINTER(vp), i64, i32, i32, i32, i32,
                                           ctypes.POINTER(CommOps)]),
@@ -162,6 +174,9 @@ def _lib() -> ctypes.CDLL:
                                          ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                          ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
             "lsb_get_exchange_bytes": (i32, [vp, P64, P64, P64]),
+            "lsb_get_exchange_stats": (i32, [vp, ctypes.POINTER(ExchangeStats)]),
+            "lsb_get_pass_exchange": (i32, [vp, i32, P64, ctypes.POINTER(ctypes.c_double),
+                                            ctypes.POINTER(ctypes.c_double)]),
             "lsb_build_info": (cp, []),
             "lsb_plan_exchange": (i32, [i64, i32, i32, i32, vp, vp, vp, vp, vp, vp]),
             "lsb_plan_exchange_device": (i32, [i32, i64, i32, i32, i32, vp, vp, vp, vp, vp, vp]),
@@ -196,13 +211,27 @@ def build_info() -> dict:
     return dict(kv.split("=", 1) for kv in info.split())
 
 
+def source_files() -> list:
+    """The library's sources, in the order the Makefile hashes them (its
+    SOURCES line, with the RT list of runtime units expanded)."""
+    import re
+    mk = open(os.path.join(ROOT_DIR, "Makefile")).read()
+    rt = re.search(r"^RT\s*:=\s*(.*)$", mk, re.M).group(1).split()
+    files = []
+    for tok in re.search(r"^SOURCES\s*:=\s*(.*)$", mk, re.M).group(1).split():
+        if tok.startswith("$(RT:"):
+            files += [f"csrc/{u}.cpp" for u in rt]
+        else:
+            files.append(tok)
+    return files
+
+
 def source_digest() -> str:
     """sha256 of the library's sources as they are in this tree, in the
     order the Makefile hashes them (SOURCES)."""
     import hashlib
     h = hashlib.sha256()
-    for rel in ("csrc/lsb_kernels.hip", "csrc/lsb_merge.hip", "csrc/lsb_segsort.hip", "csrc/lsb_runtime.cpp",
-                "csrc/lsb_kernels.h", "csrc/lsb_device.h", "../include/lsb.h"):
+    for rel in source_files():
         with open(os.path.join(ROOT_DIR, rel), "rb") as f:
             h.update(f.read())
     return h.hexdigest()
@@ -454,10 +483,26 @@ class World:
                                              *[ctypes.byref(x) for x in ms]), "lsb_get_pass_stats")
             if sh.value < 0:
                 continue
+            xb, wire, tail = ctypes.c_int64(), ctypes.c_double(), ctypes.c_double()
+            _check(_lib().lsb_get_pass_exchange(self._h, p, ctypes.byref(xb), ctypes.byref(wire),
+                                                ctypes.byref(tail)), "lsb_get_pass_exchange")
             out.append({"pass": p, "shift": int(sh.value), "launches": int(la.value), "elems": int(el.value),
                         "ms_count": ms[0].value, "ms_scatter": ms[1].value, "ms_exchange": ms[2].value,
-                        "ms_place": ms[3].value})
+                        "ms_place": ms[3].value, "exchange_bytes": int(xb.value), "ms_wire": wire.value,
+                        "ms_place_tail": tail.value})
         return out
+
+    def exchange_stats(self) -> dict:
+        """lsb_get_exchange_stats: the exchange steps since the last reset
+        (bytes per peer, wire / plan / placement / tail ms, placement bytes)."""
+        st = ExchangeStats()
+        _check(_lib().lsb_get_exchange_stats(self._h, ctypes.byref(st)), "lsb_get_exchange_stats")
+        return {"exchanges": int(st.exchanges), "calls": int(st.calls),
+                "sent_bytes": [int(x) for x in st.sent_bytes[:self.P]],
+                "recv_bytes": [int(x) for x in st.recv_bytes[:self.P]],
+                "wire_ms": st.wire_ms, "plan_ms": st.plan_ms, "place_ms": st.place_ms,
+                "place_tail_ms": st.place_tail_ms, "place_bytes": int(st.place_bytes),
+                "placed_records": int(st.placed_records), "counted_records": int(st.counted_records)}
 
     def reset_kernel_stats(self) -> None:
         _check(_lib().lsb_reset_kernel_stats(self._h), "lsb_reset_kernel_stats")

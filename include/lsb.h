@@ -66,7 +66,12 @@ typedef struct lsb_ctx lsb_ctx_t;
 #define LSB_K_PLACE     4  /* received runs -> final local slots          */
 #define LSB_K_SORT      5  /* whole lsb_sort()                            */
 #define LSB_K_SEGSORT   6  /* segmented local sort (LSB_OPT_HYBRID)       */
-#define LSB_K_COUNT     7
+#define LSB_K_WIRE      7  /* the element all-to-all calls alone (RCCL,
+                              host ops, or loopback device copies)        */
+#define LSB_K_PLACE_TAIL 8 /* placement still running after the last slice
+                              arrived (rank's stream waiting on it)       */
+#define LSB_K_COUNT     9
+#define LSB_MAX_RANKS  64  /* ranks of a context */
 
 /* Options for lsb_set_option(). */
 #define LSB_OPT_TIMING          0  /* 1: record HIP events around every kernel */
@@ -123,6 +128,11 @@ typedef struct lsb_ctx lsb_ctx_t;
                                       the plan's piece table: no placement pass (k_place's
                                       16 B of writes per record) before it; 0 places every
                                       exchange.  Same output. */
+#define LSB_OPT_FAIL_ONESWEEP   11 /* tests (fault injection): n >= 1 makes the n-th k_onesweep
+                                      launch from now fail with LSB_ERR_HIP before it is queued,
+                                      as a failed launch would; 0 (default) off.  The context
+                                      stays usable: its buffers keep their roles and the next
+                                      sort starts from the input still in A. */
 
 /* ---- geometry: DistributedArray::create (mpi/mpi_lsbsort.cpp:144-149) ---- */
 int64_t lsb_per_rank(int64_t n_total, int num_ranks);            /* ceil(n/P) */
@@ -142,6 +152,10 @@ int64_t lsb_here(int64_t n_total, int num_ranks, int rank);      /* clamp(n - r*
  * output again; one exchange per sort instead of 64 / radix_bits. */
 int  lsb_create(lsb_ctx_t** ctx, int64_t n_total, int num_ranks,
                 const int* dev_ids, int radix_bits);
+/* HIP devices this process can see (hipGetDeviceCount; 0 when there is
+ * none).  For a binding that maps one rank per GPU, e.g. the mySort stub of
+ * INTEGRATION.md (rank r on device r % count). */
+int  lsb_device_count(int* count);
 /* RCCL bootstrap: rank 0 calls this and ships the bytes to the other ranks
  * (bench.py uses torch.distributed; hip_lsbsort uses a pipe). */
 int  lsb_get_unique_id(unsigned char id[LSB_UNIQUE_ID_BYTES]);
@@ -253,6 +267,38 @@ int  lsb_get_pass_stats(lsb_ctx_t* ctx, int pass, int* shift, int64_t* launches,
  * LSB_OPT_EXCHANGE_SELF is on) and the largest one call sent.  Loopback
  * contexts (device copies) report 0. */
 int  lsb_get_exchange_bytes(lsb_ctx_t* ctx, int64_t* calls, int64_t* bytes, int64_t* max_call_bytes);
+/* The exchange steps since the last lsb_reset_kernel_stats, this context's
+ * local ranks summed: the xGMI side of a pass that SURVEY §8(d) asks to
+ * report beside the local passes (the reference's all-to-all and placement,
+ * mpi/mpi_lsbsort.cpp:562-575).  Bytes are the element collective's payload
+ * (ncclAllToAllv / grouped send-recv / the caller's alltoallv; the self
+ * segment only with LSB_OPT_EXCHANGE_SELF; loopback device copies count 0),
+ * per peer.  Times need LSB_OPT_TIMING (HIP events):
+ *   wire_ms       the all-to-all calls on the rank's stream (LSB_K_WIRE);
+ *   plan_ms       counts all-gather + device plan + tile descriptors, or the
+ *                 whole key's splitter search (LSB_K_EXCHANGE);
+ *   place_ms      the placement stream: k_place, or the merge (LSB_K_PLACE);
+ *   place_tail_ms placement still running once the last slice had arrived
+ *                 (LSB_K_PLACE_TAIL): the part not overlapped with the wire.
+ * place_bytes: algorithmic bytes of the placement kernels: 32 per placed
+ * record (16 read + 16 written), 16 per record a count-only k_place reads,
+ * 32 per record per merge level. */
+typedef struct lsb_exchange_stats {
+  int64_t exchanges;                   /* exchange steps (digits, or 1 per whole-key sort) */
+  int64_t calls;                       /* all-to-all calls (slices) */
+  int64_t sent_bytes[LSB_MAX_RANKS];   /* payload to each destination rank */
+  int64_t recv_bytes[LSB_MAX_RANKS];   /* payload from each source rank */
+  double wire_ms, plan_ms, place_ms, place_tail_ms;
+  int64_t place_bytes;
+  int64_t placed_records;              /* records written by the placement */
+  int64_t counted_records;             /* records only counted (gathered passes follow) */
+} lsb_exchange_stats_t;
+int  lsb_get_exchange_stats(lsb_ctx_t* ctx, lsb_exchange_stats_t* out);
+/* Per local pass (as lsb_get_pass_stats files an exchange under the local
+ * pass before it): payload bytes handed to the all-to-all, its wire time and
+ * the placement tail, summed since the last reset. */
+int  lsb_get_pass_exchange(lsb_ctx_t* ctx, int pass, int64_t* bytes, double* wire_ms,
+                           double* place_tail_ms);
 
 /* ---- build --------------------------------------------------------------- */
 /* "sha256=<digest of the sources the library was built from> host=<build

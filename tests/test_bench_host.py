@@ -56,7 +56,42 @@ def test_self_launch_relays_rank0_line():
     assert out["launcher"].startswith("bench.py started 3 rank processes")
     # the whole-key extra ran in its own rank processes, with the 64-bit digit
     assert out["whole_key_melem_s"] == 3 * 64 and out["whole_key_verified"] is True
+    # so did the peer-store extra, with the headline's 16-bit digits
+    assert out["peer_melem_s"] == 3 * 16 and out["peer_verified"] is True
+    assert out["peer_exchange_roofline"]["bound"] == "xgmi"
     assert out["cpu_baseline"] is None
+
+
+def test_exchange_roofline_keys():
+    """N > 1: the line carries the exchange side of SURVEY 8(d) (bench.py
+    exchange_roofline, here from dry_stats' made-up per-rank bytes: rank r
+    sends (r + 1) MiB per peer per exchange, 4 exchanges per sort)."""
+    r = _bench(["--gpus", "3", "--dry-rank", "--no-cpu-baseline", "--no-extras", "--steps", "2"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    x = _line(r.stdout)["exchange_roofline"]
+    assert x["bound"] == "xgmi" and x["unit"] == "GB/s" and x["peak"] == 153.0 and "spec" in x["peak_source"]
+    assert x["exchanges_per_sort"] == 4
+    mib = 1 << 20
+    assert x["link_bytes_per_exchange"] == {"max": 3 * mib, "min": mib}
+    assert x["link_bytes_per_sort"]["max_link"][0] == 2 and x["link_bytes_per_sort"]["min_link"][0] == 0
+    assert x["link_bytes_per_sort"]["max_over_min"] == 3.0
+    assert x["rank_bytes_per_sort"] == {"max": 2 * 4 * 3 * mib, "min": 2 * 4 * mib}
+    # wire: 1 ms per exchange -> the busiest link moved 12 MiB in 4 ms
+    assert x["wire_ms_per_sort"]["max"] == 4.0
+    assert x["achieved"] == round(12 * mib / 4e-3 / 1e9, 2)
+    assert x["frac"] == round(x["achieved"] / 153.0, 4)
+    assert x["link_bound_ms_per_sort"] == round(12 * mib / 153e9 * 1e3, 3)
+    p = x["place"]
+    assert p["tail_ms_per_sort"] == 0.5 and p["ms_per_sort"] == 2.0 and p["overlapped_frac"] == 0.75
+    assert p["placed_records_per_sort"] == 1000 and p["counted_records_per_sort"] == 3000
+
+
+def test_peer_failure_keeps_the_headline():
+    r = _bench(["--gpus", "2", "--dry-rank", "--dry-fail-peer", "1", "--no-cpu-baseline"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = _line(r.stdout)
+    assert out["value"] == 2 * 16 and out["whole_key_melem_s"] == 2 * 64
+    assert "peer_melem_s" not in out and "rank exit codes" in out["peer_error"]
 
 
 def test_self_launch_fails_with_the_failing_rank():
@@ -72,6 +107,7 @@ def test_whole_key_failure_keeps_the_headline():
     out = _line(r.stdout)
     assert out["value"] == 2 * 16 and "whole_key_melem_s" not in out
     assert "whole_key_error" in out and "rank exit codes" in out["whole_key_error"]
+    assert out["peer_melem_s"] == 2 * 16
 
 
 @pytest.mark.parametrize("fail_extra", [False, True])
@@ -94,3 +130,4 @@ def test_torchrun_ranks_run_the_extra_in_child_processes(fail_extra):
         assert "whole_key_error" in out and "whole_key_melem_s" not in out
     else:
         assert out["whole_key_melem_s"] == 128.0
+    assert out["peer_melem_s"] == 32.0 and out["exchange_roofline"]["exchanges_per_sort"] == 4

@@ -380,6 +380,48 @@ def test_rccl_world_of_one(lsb_built, oracle_mod, digests, p2p):
         w.close()
 
 
+@pytest.mark.parametrize("bits,slices", [(16, 4), (8, 3), (64, 5)])
+def test_exchange_stats_world_of_one(lsb_built, oracle_mod, digests, bits, slices):
+    """lsb_get_exchange_stats through real RCCL: a world of one with the
+    exchange forced and the self segment sent through ncclAllToAllv, so every
+    record crosses the collective once per exchange digit (16 B each), in
+    `slices` calls; the wire, plan, placement and tail times are timed and
+    the placement bytes follow the gathered-pass rule (the last exchange
+    places, 32 B per record; the others count, 16 B).  The whole key: one
+    exchange, one merge level (a single run is copied)."""
+    d = next(r for r in digests["rows"] if r["P"] == 1)
+    n = d["n"]
+    w = lsb_built.World.rank(n, 1, 0, 0, lsb_built.get_unique_id(), radix_bits=bits)
+    try:
+        w.set_option(lsb_built.OPT_FORCE_EXCHANGE, 1)
+        w.set_option(lsb_built.OPT_EXCHANGE_SELF, 1)
+        w.set_option(lsb_built.OPT_EXCHANGE_SLICES, slices)
+        w.generate()
+        w.reset_kernel_stats()
+        w.set_timing(True)
+        w.my_sort()
+        w.sync()
+        x = w.exchange_stats()
+        assert oracle_mod.digest(w.copy_out(0)) == d["output"]
+        ex = 1 if bits == 64 else 64 // bits
+        assert x["exchanges"] == ex and x["calls"] == ex * slices
+        assert x["sent_bytes"] == [16 * n * ex] and x["recv_bytes"] == [16 * n * ex]
+        assert x["wire_ms"] > 0 and x["plan_ms"] > 0 and x["place_ms"] > 0 and x["place_tail_ms"] >= 0
+        if bits == 64:
+            assert x["placed_records"] == n and x["place_bytes"] == 32 * n  # one level: the single run copied
+        else:
+            assert x["placed_records"] == n and x["counted_records"] == n * (ex - 1)
+            assert x["place_bytes"] == 32 * n + 16 * n * (ex - 1)
+            rows = w.pass_stats()
+            xrows = [r for r in rows if r["exchange_bytes"]]
+            assert len(xrows) == ex and all(r["exchange_bytes"] == 16 * n for r in xrows)
+            assert all(r["ms_wire"] > 0 and r["ms_exchange"] >= r["ms_wire"] for r in xrows)
+        w.reset_kernel_stats()
+        assert w.exchange_stats()["sent_bytes"] == [0]
+    finally:
+        w.close()
+
+
 @pytest.mark.parametrize("onesweep", [1, 0])
 def test_kernel_stats(lsb_built, onesweep):
     with lsb_built.World(1 << 20, ranks=1) as w:

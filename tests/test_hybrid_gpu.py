@@ -215,3 +215,29 @@ def test_option_range(lsb_built):
     with lsb_built.World(10, ranks=1) as w:
         with pytest.raises(lsb_built.LsbError):
             w.set_option(lsb_built.OPT_HYBRID, 3)
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("fail_at", [1, 2, 3])
+def test_failed_launch_mid_hybrid_keeps_the_context(lsb_built, oracle_mod, mode, fail_at):
+    """A k_onesweep launch that fails inside the hybrid (LSB_OPT_FAIL_ONESWEEP
+    injects it: 300,007 records take k = 3 byte passes) returns the error and
+    leaves the context whole (advisor r03): A again holds the input, A, B and
+    R are three distinct buffers, so the next sort on the same context sorts
+    that input exactly, later sorts too, and the context closes cleanly."""
+    n = 300_007
+    with lsb_built.World(n, ranks=1) as w:
+        w.set_option(lsb_built.OPT_HYBRID, mode)
+        w.generate()
+        inp = w.gather_global()
+        w.set_option(lsb_built.OPT_FAIL_ONESWEEP, fail_at)
+        with pytest.raises(lsb_built.LsbError, match="injected"):
+            w.my_sort()
+        assert np.array_equal(w.gather_global(), inp)
+        w.my_sort()
+        assert np.array_equal(w.gather_global(), oracle_mod.stable_sort(inp))
+        assert w.verify() == (True, -1)
+        for _ in range(2):  # the buffers keep rotating without aliasing
+            w.generate()
+            w.my_sort()
+            assert w.verify() == (True, -1)

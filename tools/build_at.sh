@@ -8,21 +8,19 @@ set -euo pipefail
 rev=$1; out=$2; shift 2
 R=$(cd "$(dirname "$0")/.." && pwd)
 mkdir -p "$out/src/distributed-lsb_amd/csrc" "$out/src/include"
-for f in distributed-lsb_amd/csrc/lsb_kernels.hip distributed-lsb_amd/csrc/lsb_merge.hip \
-         distributed-lsb_amd/csrc/lsb_segsort.hip \
-         distributed-lsb_amd/csrc/lsb_runtime.cpp distributed-lsb_amd/csrc/lsb_kernels.h distributed-lsb_amd/csrc/lsb_device.h include/lsb.h; do
-  git -C "$R" show "$rev:$f" > "$out/src/$f" 2>/dev/null || rm -f "$out/src/$f"  # older revisions lack some
+git -C "$R" show "$rev:include/lsb.h" > "$out/src/include/lsb.h"
+for f in $(git -C "$R" ls-tree --name-only "$rev" distributed-lsb_amd/csrc/); do
+  git -C "$R" show "$rev:$f" > "$out/src/$f"
 done
 S=$out/src
 H=/opt/rocm/bin/hipcc
 F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -I$S/include -I$S/distributed-lsb_amd/csrc $*"
-$H $F -c "$S/distributed-lsb_amd/csrc/lsb_kernels.hip" -o "$out/k.o"
-$H $F -c "$S/distributed-lsb_amd/csrc/lsb_merge.hip" -o "$out/m.o"
-objs=("$out/k.o" "$out/m.o")
-if [ -f "$S/distributed-lsb_amd/csrc/lsb_segsort.hip" ]; then
-  $H $F -c "$S/distributed-lsb_amd/csrc/lsb_segsort.hip" -o "$out/s.o"
-  objs+=("$out/s.o")
-fi
-$H $F -c "$S/distributed-lsb_amd/csrc/lsb_runtime.cpp" -o "$out/r.o"
-$H --offload-arch=gfx950 -shared -o "$out/liblsb.so" "${objs[@]}" "$out/r.o" -L/opt/rocm/lib -lrccl \
+objs=()
+for src in "$S"/distributed-lsb_amd/csrc/*.hip "$S"/distributed-lsb_amd/csrc/*.cpp; do
+  o="$out/$(basename "${src%.*}").o"
+  $H $F -c "$src" -o "$o" &
+  objs+=("$o")
+done
+wait
+$H --offload-arch=gfx950 -shared -o "$out/liblsb.so" "${objs[@]}" -L/opt/rocm/lib -lrccl \
   -Wl,-rpath,/opt/rocm/lib

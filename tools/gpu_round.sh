@@ -14,6 +14,7 @@
 #             summarise with tools/pmc_summary.py TAG_hybrid gpurun_out/prof_hybrid ... --templates)
 #   sq        tools/sq_counters.sh: SQ counters of the sort at 2^28
 #   stress    tools/stress_mix.py for STRESS_S seconds (default 150): random sorts, 0 wrong
+#   dropin    tests/test_dropin_gpu.py alone (the reference program with its mySort on the library)
 # Output under gpurun_out/$TAG/.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -65,6 +66,10 @@ for s in $RUN; do
         > $O/stress_mix.log 2>&1 || fail stress $O/stress_mix.log
       tail -1 $O/stress_mix.log
       grep -q "done: 0 of" $O/stress_mix.log || fail stress $O/stress_mix.log ;;
+    dropin)
+      timeout -k 10 400 python -u -m pytest tests/test_dropin_gpu.py -m gpu -x -v --timeout 240 \
+        --timeout-method thread > $O/dropin.log 2>&1 || fail dropin $O/dropin.log
+      tail -2 $O/dropin.log ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

@@ -1,6 +1,6 @@
 // ASan/UBSan driver for the C ABI's host code (sanitizers on host
 // code).  `make -C distributed-lsb_amd asan` links it against an ASan/UBSan
-// build of lsb_runtime.cpp (device code unchanged) and runs it without a GPU:
+// build of the runtime units (csrc/lsb_*.cpp; device code unchanged) and runs it without a GPU:
 //   - lsb_plan_exchange on random, skewed, empty and n < P count matrices:
 //     conservation (sum send = sum recv = here), displacement prefix sums,
 //     every live placement offset inside [0, here);

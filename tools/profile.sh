@@ -13,8 +13,10 @@ STEPS=${STEPS:-3}
 EXTRA=${BENCH_ARGS:-}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-BENCH="$REPO/bench.py --steps $STEPS --warmup 1 --no-cpu-baseline --no-traffic $EXTRA"
+# --no-extras: no second GPU process (the hybrid extra) under the profiler;
+# profile the hybrid explicitly with BENCH_ARGS="--passes hybrid".
+BENCH="$REPO/bench.py --steps $STEPS --warmup 1 --no-cpu-baseline --no-traffic --no-extras $EXTRA"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o run -- python3 $BENCH > "$OUT/stats.log" 2>&1
-timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- python3 $REPO/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-traffic $EXTRA > "$OUT/fetch.log" 2>&1
-timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- python3 $REPO/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-traffic $EXTRA > "$OUT/write.log" 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- python3 $REPO/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-traffic --no-extras $EXTRA > "$OUT/fetch.log" 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- python3 $REPO/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-traffic --no-extras $EXTRA > "$OUT/write.log" 2>&1
 find "$OUT" -name "*.csv" | sort
