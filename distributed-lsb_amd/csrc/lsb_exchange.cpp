@@ -454,7 +454,13 @@ bool exchange_onesweep_applies(const lsb_ctx* c) {
 // byte at `next` over the output (the next local pass follows directly).
 int local_pass_os(lsb_ctx* c, Rank& r, int shift, int next, lsb::OnesweepExtra extra) {
   HIP_TRY(hipSetDevice(r.dev));
-  extra.halves = r.os_halves;
+  // A gathered pass always takes the whole stage: the split stage's gathered
+  // instances spill (168 VGPRs at 3 workgroups per CU: 160-236 B per lane),
+  // while the whole stage's fit (128 VGPRs, no or 12 B of spill) and cost
+  // skewed keys ~1 % per pass against the split (58.53 vs 59.24 ms per Zipf
+  // sort, profiles/ab/r02_ab28_zipf_stage.log) -- far less than the placement
+  // the gathered pass saves (32 B per record).
+  extra.halves = r.gather_pending ? 1 : r.os_halves;
   r.starts_fused = false;
   const int64_t m = r.here;
   if (m == 0) {
@@ -566,8 +572,8 @@ int sort_exchange_onesweep(lsb_ctx* c) {
     if (!st.exch) continue;
     for (Rank& r : c->ranks) {
       r.place_next = c->peer || r.here == 0 ? -1 : after;
-      // Not with the split stage (skewed keys): its gathered instances spill.
-      r.gather_next = c->gather && r.place_next >= 0 && r.os_halves == 1;
+      // Skewed keys too: their gathered pass takes the whole stage (local_pass_os).
+      r.gather_next = c->gather && r.place_next >= 0;
       r.place_hist = nullptr;
       if (r.place_next >= 0) {
         r.place_hist = r.os_hist + (size_t)(r.os_cur ^ 1) * lsb::kOnesweepSubs * lsb::kBuckets;

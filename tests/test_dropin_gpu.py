@@ -42,7 +42,7 @@ def _run(n, P, radix=None, timeout=240):
 
 
 @pytest.mark.parametrize("n,P,radix", [
-    (1000003, 1, None), (1000000, 2, None), (1000003, 4, None), (100003, 4, 8), (1000, 3, 64),
+    (1048576, 1, None), (1000000, 2, None), (1000003, 4, None), (100003, 4, 8), (1000, 3, 64),
     (7, 2, None), (3, 4, None), (0, 2, None),
 ])
 def test_reference_program_sorts_through_the_stub(lsb_built, ref_vectors, n, P, radix):

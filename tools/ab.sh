@@ -11,6 +11,7 @@
 #   uniform      the LSD sort of the PCG input
 #   zipf         Zipf (s = 1.1) keys                      (LSB_DIST=zipf)
 #   x16          the per-digit exchange at P = 1, 16-bit  (LSB_FORCE_EXCHANGE=1 LSB_RADIX_BITS=16)
+#   x16zipf      the same with Zipf keys; -g0 suffix: LSB_GATHER=0 (placement at every exchange)
 #   hybrid       the hybrid local sort                    (LSB_PASSES=hybrid)
 #   reduce-scan  count + scan + scatter passes            (LSB_PASSES=reduce-scan)
 # Each round runs every build once per form, alternating the build order so
@@ -37,6 +38,9 @@ form_env() {
     uniform) echo "" ;;
     zipf) echo "LSB_DIST=zipf" ;;
     x16) echo "LSB_FORCE_EXCHANGE=1 LSB_RADIX_BITS=16" ;;
+    x16-g0) echo "LSB_FORCE_EXCHANGE=1 LSB_RADIX_BITS=16 LSB_GATHER=0" ;;
+    x16zipf) echo "LSB_DIST=zipf LSB_FORCE_EXCHANGE=1 LSB_RADIX_BITS=16" ;;
+    x16zipf-g0) echo "LSB_DIST=zipf LSB_FORCE_EXCHANGE=1 LSB_RADIX_BITS=16 LSB_GATHER=0" ;;
     hybrid) echo "LSB_PASSES=hybrid" ;;
     reduce-scan) echo "LSB_PASSES=reduce-scan" ;;
     *) echo "unknown form $1" >&2; exit 2 ;;

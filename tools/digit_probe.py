@@ -27,7 +27,7 @@ w.set_option(lsbsort.OPT_ONESWEEP, 0 if os.environ.get("LSB_PASSES") == "reduce-
 # LSB_PASSES=hybrid: k top-byte passes + the segmented local sort (LSB_OPT_HYBRID)
 w.set_option(lsbsort.OPT_HYBRID, {"hybrid": 1, "hybrid-segsort": 2}.get(os.environ.get("LSB_PASSES", ""), 0))
 w.set_timing(True)
-names = ["upsweep", "scan", "scatter", "exchange", "place", "segsort", "sort"]
+names = ["upsweep", "scan", "scatter", "exchange", "wire", "place", "place_tail", "segsort", "sort"]
 for rep in range(2):
     w.generate(DIST)
     w.my_sort()

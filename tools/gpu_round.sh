@@ -70,6 +70,13 @@ for s in $RUN; do
       timeout -k 10 400 python -u -m pytest tests/test_dropin_gpu.py -m gpu -x -v --timeout 240 \
         --timeout-method thread > $O/dropin.log 2>&1 || fail dropin $O/dropin.log
       tail -2 $O/dropin.log ;;
+    allocbw)  # buffer-placement probe: 3 fresh processes, then one pooled allocation
+      [ -x tools/kbench/allocbw ] || fail allocbw /dev/null
+      for k in 1 2 3; do
+        timeout -k 10 120 tools/kbench/allocbw 4 30 5 > $O/allocbw_$k.log 2>&1 || fail allocbw $O/allocbw_$k.log
+      done
+      timeout -k 10 120 tools/kbench/allocbw 4 30 5 1 > $O/allocbw_pool.log 2>&1 || fail allocbw $O/allocbw_pool.log
+      grep -h "buffer .: read\|runs" $O/allocbw_*.log | head -60 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
