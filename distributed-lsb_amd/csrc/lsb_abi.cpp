@@ -474,6 +474,18 @@ int lsb_get_exchange_stats(lsb_ctx_t* c, lsb_exchange_stats_t* out) {
   return LSB_OK;
 }
 
+int lsb_get_placement(lsb_ctx_t* c, int rank, int* candidates, double* chosen_ms, double* first_pair_ms,
+                      double* worst_ms) {
+  LSB_TRY(check_ctx(c));
+  Rank* r = local_rank(c, rank);
+  if (!r) return fail(LSB_ERR_INVALID, "lsb_get_placement", "rank");
+  if (candidates) *candidates = r->placement_k;
+  if (chosen_ms) *chosen_ms = r->placement_ms[0];
+  if (first_pair_ms) *first_pair_ms = r->placement_ms[1];
+  if (worst_ms) *worst_ms = r->placement_ms[2];
+  return LSB_OK;
+}
+
 int lsb_get_scatter_elems(lsb_ctx_t* c, int64_t* elems) {
   LSB_TRY(check_ctx(c));
   if (elems) *elems = c->scatter_elems;

@@ -73,6 +73,103 @@ int max_chunks_for_device(int dev) {
   return std::min(lsb::kMaxChunks, 2 * prop.multiProcessorCount);
 }
 
+// ---- record buffers A and B, placement-calibrated ----------------------------
+// How fast an LSD pass streams between two 16 GiB record buffers depends on
+// where the driver placed them.  tools/kbench/allocbw.hip, four fresh
+// processes of four 2^30-record buffers each (profiles/r04/allocbw_*.log):
+// pure streaming reads are level (2.85-3.0 ms), but the LSD write pattern
+// (256 bucket frontiers, 256-byte runs) copies X -> Y in 5.7-5.9 ms into some
+// buffers, 6.85-6.9 ms into most, and 7.2-7.3 ms between some pairs, in both
+// directions -- the same +-5 % that k_onesweep's pass times showed from
+// context to context (tools/alloc_probe.py, profiles/ab/r03_alloc_*).  So a
+// rank's A and B are chosen among K candidate buffers: each ordered pair is
+// timed with that copy (launch_probe_runs), the pair with the smallest sum of
+// both directions (the passes ping-pong) is kept, the rest are freed.  K =
+// LSB_PLACEMENT_CANDIDATES (environment, default 4; 2 or less: A and B as
+// allocated), for buffers of at least 1 GiB and only as many as fit in 90 %
+// of the free memory.  Cost at 2^30 records: ~0.2 s at context creation.
+int alloc_records(lsb_ctx* c, Rank& r) {
+  const size_t per = (size_t)c->per;
+  const double bytes = (double)per * sizeof(Elem);
+  int K = 4;
+  if (const char* e = getenv("LSB_PLACEMENT_CANDIDATES")) K = atoi(e);
+  K = std::min(K, 8);
+  size_t free_b = 0, total_b = 0;
+  if (K > 2 && bytes >= (double)(1ull << 30) && hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
+    while (K > 2 && K * bytes > 0.9 * (double)free_b) --K;
+  } else {
+    (void)hipGetLastError();
+    K = 2;
+  }
+  r.placement_k = K > 2 ? K : 0;
+  if (K <= 2) {
+    LSB_TRY(dev_alloc(&r.A, per));
+    return dev_alloc(&r.B, per);
+  }
+  std::vector<Elem*> cand;
+  for (int k = 0; k < K; ++k) {
+    Elem* p = nullptr;
+    if (dev_alloc(&p, per) != LSB_OK) break;  // fewer candidates than hoped
+    cand.push_back(p);
+  }
+  (void)hipGetLastError();
+  auto release = [&](Elem* keep0, Elem* keep1) {
+    for (Elem* p : cand)
+      if (p != keep0 && p != keep1) (void)hipFree(p);
+  };
+  if (cand.size() < 2) {
+    release(nullptr, nullptr);
+    return fail(LSB_ERR_NOMEM, "alloc_records", "record buffers");
+  }
+  K = (int)cand.size();
+  r.placement_k = K;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  std::vector<double> ms((size_t)K * K, 0.0);
+  hipError_t err = hipEventCreate(&e0);
+  if (err == hipSuccess) err = hipEventCreate(&e1);
+  if (err == hipSuccess) err = lsb::launch_probe_runs(cand[0], cand[1], c->per, r.stream);  // warm-up
+  for (int x = 0; x < K && err == hipSuccess; ++x)
+    for (int y = 0; y < K && err == hipSuccess; ++y) {
+      if (x == y) continue;
+      float best = 1e30f;
+      for (int rep = 0; rep < 2 && err == hipSuccess; ++rep) {
+        err = hipEventRecord(e0, r.stream);
+        if (err == hipSuccess) err = lsb::launch_probe_runs(cand[x], cand[y], c->per, r.stream);
+        if (err == hipSuccess) err = hipEventRecord(e1, r.stream);
+        if (err == hipSuccess) err = hipEventSynchronize(e1);
+        float t = 0.f;
+        if (err == hipSuccess) err = hipEventElapsedTime(&t, e0, e1);
+        best = std::min(best, t);
+      }
+      ms[(size_t)x * K + y] = best;
+    }
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  if (err != hipSuccess) {
+    release(nullptr, nullptr);
+    return fail(LSB_ERR_HIP, "alloc_records: placement probe", hipGetErrorString(err));
+  }
+  int bx = 0, by = 1;
+  double best = 1e300, worst = 0.0;
+  for (int x = 0; x < K; ++x)
+    for (int y = x + 1; y < K; ++y) {
+      const double pair = 0.5 * (ms[(size_t)x * K + y] + ms[(size_t)y * K + x]);
+      if (pair < best) {
+        best = pair;
+        bx = x;
+        by = y;
+      }
+      worst = std::max(worst, pair);
+    }
+  r.placement_ms[0] = best;
+  r.placement_ms[1] = 0.5 * (ms[1] + ms[(size_t)K]);  // the first two buffers allocated
+  r.placement_ms[2] = worst;
+  r.A = cand[bx];
+  r.B = cand[by];
+  release(r.A, r.B);
+  return LSB_OK;
+}
+
 int init_rank(lsb_ctx* c, Rank& r, int rank, int dev) {
   r.rank = rank;
   r.dev = dev;
@@ -82,12 +179,10 @@ int init_rank(lsb_ctx* c, Rank& r, int rank, int dev) {
   HIP_TRY(hipStreamCreateWithFlags(&r.pstream, hipStreamNonBlocking));
   HIP_TRY(hipEventCreateWithFlags(&r.pevent, hipEventDisableTiming));
   HIP_TRY(hipEventCreateWithFlags(&r.pdone, hipEventDisableTiming));
-  const size_t per = (size_t)c->per;
   r.chunking = lsb::make_chunking(r.here, max_chunks_for_device(dev));
   const size_t hist_entries = (size_t)lsb::kBuckets * std::max(1, r.chunking.num_chunks);
   const size_t P = (size_t)c->P, nb = (size_t)c->nb;
-  LSB_TRY(dev_alloc(&r.A, per));
-  LSB_TRY(dev_alloc(&r.B, per));
+  LSB_TRY(alloc_records(c, r));
   r.buf[0] = r.A;
   r.buf[1] = r.B;
   // R (the all-to-all receive buffer) is allocated on first use: a context

@@ -1720,6 +1720,21 @@ __global__ __launch_bounds__(256) void k_check_sorted(const Elem* __restrict__ A
   }
 }
 
+// Buffer-placement probe (launch_probe_runs): record i = (tile t, slot j)
+// of `in` goes to bucket b = j / 16 of `out`, at b * (m / 256) + t * 16 +
+// j % 16: every 4096-record tile sends one 256-byte run to each of 256 bucket
+// frontiers, the write pattern of an LSD pass, with sequential reads.
+__global__ __launch_bounds__(256) void k_probe_runs(const Elem* __restrict__ in, Elem* __restrict__ out,
+                                                    int64_t m) {
+  const int64_t per_bucket = m / kBuckets;
+  const int64_t n = per_bucket * kBuckets;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t t = i >> 12;
+    const int j = (int)(i & (kTile - 1));
+    store_elem(out + (int64_t)(j >> 4) * per_bucket + t * 16 + (j & 15), load_elem_nt(in + i));
+  }
+}
+
 int grid_for(int64_t work, int block, int cap) {
   const int64_t g = (work + block - 1) / block;
   return (int)(g < 1 ? 1 : (g > cap ? cap : g));
@@ -1863,7 +1878,11 @@ hipError_t launch_onesweep(const Elem* in, Elem* out, int64_t m, int shift, int 
   if (e != hipSuccess) return e;
   const int64_t TT = (m + kTile - 1) / kTile;
   auto* c16 = reinterpret_cast<unsigned long long*>(extra.count16);
-  // The split stage only for the plain and next-digit forms.
+  const bool gat = extra.gather != nullptr;
+  // The split stage only for the plain and next-digit forms, never gathered
+  // (its gathered instances spill: 160-236 B per lane at 168 VGPRs; a
+  // gathered pass takes the whole stage, lsb_exchange.cpp local_pass_os).
+  if (extra.halves == 2 && gat) return hipErrorInvalidValue;
   const bool split = extra.halves == 2 && c16 == nullptr;
   // Persistent grid (`grid` = 2 workgroups per CU; 3 with the split stage),
   // a multiple of the XCD count; no more than the tiles.
@@ -1873,7 +1892,6 @@ hipError_t launch_onesweep(const Elem* in, Elem* out, int64_t m, int shift, int 
   const dim3 gd((unsigned)g), bd(split ? kOsSplitBlock : kOsBlock);
   uint32_t* st = status;
   const GatherSrc gsrc = extra.gather ? *extra.gather : GatherSrc();
-  const bool gat = extra.gather != nullptr;
   // One launch of the instance, gathered or not.
   auto go = [&](auto kplain, auto kgather, int nshift, uint32_t* nhist, unsigned long long* cnt16,
                 SegPass sp) {
@@ -1899,16 +1917,15 @@ hipError_t launch_onesweep(const Elem* in, Elem* out, int64_t m, int shift, int 
   } else if (next_shift >= 0) {
     e = hipMemsetAsync(next_hist, 0, sizeof(uint32_t) * kSub * kBuckets, s);
     if (e != hipSuccess) return e;
-    if (split)
+    if (split)  // never gathered (checked above)
       go(k_onesweep<kOsSplitBlock, kOsSplitIpt, true, false, 2>,
-         k_onesweep<kOsSplitBlock, kOsSplitIpt, true, false, 2, false, true>, next_shift, next_hist, nullptr,
-         SegPass());
+         k_onesweep<kOsSplitBlock, kOsSplitIpt, true, false, 2>, next_shift, next_hist, nullptr, SegPass());
     else
       go(k_onesweep<kOsBlock, kOsIpt, true, false, 1>, k_onesweep<kOsBlock, kOsIpt, true, false, 1, false, true>,
          next_shift, next_hist, nullptr, SegPass());
-  } else if (split) {
+  } else if (split) {  // never gathered (checked above)
     go(k_onesweep<kOsSplitBlock, kOsSplitIpt, false, false, 2>,
-       k_onesweep<kOsSplitBlock, kOsSplitIpt, false, false, 2, false, true>, 0, nullptr, nullptr, SegPass());
+       k_onesweep<kOsSplitBlock, kOsSplitIpt, false, false, 2>, 0, nullptr, nullptr, SegPass());
   } else {
     go(k_onesweep<kOsBlock, kOsIpt, false, false, 1>, k_onesweep<kOsBlock, kOsIpt, false, false, 1, false, true>,
        0, nullptr, nullptr, SegPass());
@@ -2023,6 +2040,12 @@ hipError_t launch_verify(const Elem* A, int64_t here, int64_t gbase, int64_t n, 
   if (here <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_verify, dim3(grid_for(here, 256, 8192)), dim3(256), 0, s, A, here, gbase, n,
                      per, gen, first_bad);
+  return hipGetLastError();
+}
+
+hipError_t launch_probe_runs(const Elem* in, Elem* out, int64_t m, hipStream_t s) {
+  if (m < (int64_t)kTile * kBuckets) return hipErrorInvalidValue;  // >= 16 records per run and bucket
+  hipLaunchKernelGGL(k_probe_runs, dim3(8192), dim3(256), 0, s, in, out, m);
   return hipGetLastError();
 }
 

@@ -52,6 +52,11 @@ struct Rank {
   Elem* A = nullptr;  // per slots: input / output (DistributedArray A)
   Elem* B = nullptr;  // per slots: ping-pong partner
   Elem* R = nullptr;  // per slots: receive buffer (P > 1 only)
+  // A and B were chosen among placement_k candidate buffers (alloc_records;
+  // 0: allocated as they came): ms of the probe copy, mean of both
+  // directions, of the chosen pair, of the first two allocated, of the worst.
+  int placement_k = 0;
+  double placement_ms[3] = {0.0, 0.0, 0.0};
   uint32_t* chunk_hist = nullptr;       // [256][num_chunks]
   uint64_t* chunk_off = nullptr;        // [256][num_chunks]
   uint64_t* totals = nullptr;           // [256] local counts of the current 8-bit digit

@@ -175,6 +175,8 @@ def _lib() -> ctypes.CDLL:
                                          ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
             "lsb_get_exchange_bytes": (i32, [vp, P64, P64, P64]),
             "lsb_get_exchange_stats": (i32, [vp, ctypes.POINTER(ExchangeStats)]),
+            "lsb_get_placement": (i32, [vp, i32, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_double),
+                                        ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
             "lsb_get_pass_exchange": (i32, [vp, i32, P64, ctypes.POINTER(ctypes.c_double),
                                             ctypes.POINTER(ctypes.c_double)]),
             "lsb_build_info": (cp, []),
@@ -491,6 +493,18 @@ class World:
                         "ms_place": ms[3].value, "exchange_bytes": int(xb.value), "ms_wire": wire.value,
                         "ms_place_tail": tail.value})
         return out
+
+    def placement(self, rank: Optional[int] = None) -> dict:
+        """lsb_get_placement: how rank's A and B were chosen among candidate
+        buffers (candidates 0: allocated as they came) and the probe copy's ms
+        for the chosen pair, the first two allocated and the slowest pair."""
+        r = self.local_ranks[0] if rank is None else rank
+        k = ctypes.c_int()
+        ms = [ctypes.c_double() for _ in range(3)]
+        _check(_lib().lsb_get_placement(self._h, r, ctypes.byref(k), *[ctypes.byref(x) for x in ms]),
+               "lsb_get_placement")
+        return {"candidates": int(k.value), "chosen_ms": round(ms[0].value, 4),
+                "first_pair_ms": round(ms[1].value, 4), "worst_ms": round(ms[2].value, 4)}
 
     def exchange_stats(self) -> dict:
         """lsb_get_exchange_stats: the exchange steps since the last reset

@@ -344,7 +344,7 @@ def test_error_codes_on_a_context(lsb_built):
         assert lib.lsb_set_option(h, 99, 1) == 1
         assert lib.lsb_generate_ex(h, 7, 0.0) == 1
         assert lib.lsb_generate_ex(h, lsb_built.DIST_ZIPF, 0.0) == 1
-        assert lib.lsb_get_kernel_stats(h, 7, None, None) == 1
+        assert lib.lsb_get_kernel_stats(h, len(lsb_built.KERNEL_NAMES), None, None) == 1
         first, num = ctypes.c_int(), ctypes.c_int()
         assert lib.lsb_local_ranks(h, ctypes.byref(first), ctypes.byref(num)) == 0
         assert (first.value, num.value) == (0, 2)
@@ -713,3 +713,27 @@ def test_harness_rccl_ranks_share_gpu(lsb_built, ref_vectors, n, P, extra):
     assert "Array is sorted" in lines
     printed = [l for l in lines if l.startswith("A[")]
     assert printed == [f"A[{i}] = ({k},{v})" for i, k, v in case["input"] + case["output"]]
+
+
+# ------------------------------------------ placement-calibrated A and B
+def test_placement_calibrated_buffers(lsb_built, monkeypatch):
+    """A rank whose record buffers hold >= 1 GiB picks A and B among 4
+    candidate buffers by a probe copy (lsb_get_placement); with
+    LSB_PLACEMENT_CANDIDATES=2 it keeps the first two allocated.  Either way
+    the sort is the same (verified on device)."""
+    n = 1 << 26  # 1 GiB per buffer
+    with lsb_built.World(n, ranks=1) as w:
+        p = w.placement()
+        assert p["candidates"] == 4, p
+        assert 0 < p["chosen_ms"] <= p["first_pair_ms"] <= p["worst_ms"], p
+        w.generate()
+        w.my_sort()
+        assert w.verify() == (True, -1)
+    monkeypatch.setenv("LSB_PLACEMENT_CANDIDATES", "2")
+    with lsb_built.World(n, ranks=1) as w:
+        assert w.placement()["candidates"] == 0
+        w.generate()
+        w.my_sort()
+        assert w.verify() == (True, -1)
+    with lsb_built.World(1 << 20, ranks=1) as w:  # small buffers: as allocated
+        assert w.placement() == {"candidates": 0, "chosen_ms": 0.0, "first_pair_ms": 0.0, "worst_ms": 0.0}

@@ -10,6 +10,9 @@ ones.
 
     python tools/alloc_probe.py [LG] [CONTEXTS] [REPS]
 
+LSB_PLACEMENT_CANDIDATES=2 allocates A and B as they come; the default (4)
+picks them among 4 candidates by a probe copy (lsb_get_placement).
+
 (A build whose record buffers came from hipExtMallocWithFlags(...,
 hipDeviceMallocContiguous) ran every pass ~48 % slower, 10.3-10.9 ms:
 profiles/ab/r03_alloc_contig.log; not kept.)
@@ -47,6 +50,7 @@ for c in range(ctxs):
         w.set_timing(False)
         print(json.dumps({"context": c, "rep": r, "ms": round(ms, 2), "passes": passes}), flush=True)
     ok, _ = w.verify()
-    print(json.dumps({"context": c, "verified": ok}), flush=True)
+    print(json.dumps({"context": c, "verified": ok, "placement": w.placement(),
+                      "env_candidates": os.environ.get("LSB_PLACEMENT_CANDIDATES", "default")}), flush=True)
 for w in worlds:
     w.close()

@@ -77,6 +77,14 @@ for s in $RUN; do
       done
       timeout -k 10 120 tools/kbench/allocbw 4 30 5 1 > $O/allocbw_pool.log 2>&1 || fail allocbw $O/allocbw_pool.log
       grep -h "buffer .: read\|runs" $O/allocbw_*.log | head -60 ;;
+    placement)  # A/B: plain A/B allocation vs the calibrated choice, alternating fresh processes
+      for k in 1 2 3; do
+        for cand in 2 4; do
+          LSB_PLACEMENT_CANDIDATES=$cand timeout -k 10 200 python -u tools/alloc_probe.py 30 2 2 \
+            >> $O/placement_c$cand.log 2>&1 || fail placement $O/placement_c$cand.log
+        done
+      done
+      grep -h verified $O/placement_c*.log ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
