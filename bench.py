@@ -782,6 +782,7 @@ def main():
     scatter_elems = w.scatter_elems()
     xcalls, xbytes, _ = w.exchange_bytes()
     xstats = w.exchange_stats()
+    placement = w.placement()
     last = w.last_sort()
     w.close()
     xroof = exchange_roofline(d.all_gather_obj({"stats": xstats}), a.steps) if N > 1 else None
@@ -882,6 +883,9 @@ def main():
             "sort": "the whole sort, per rank"},
         "exchange_bytes_per_step": xbytes // a.steps if N > 1 else 0,
         "exchange_roofline": xroof,
+        "placement": dict(placement, basis="rank 0's A and B, chosen at context creation among `candidates` "
+                                            "buffers by an LSD-pattern probe copy, ms per copy (lsb_get_placement; "
+                                            "DESIGN.md 4)"),
         "verified": verified,
         "vs_baseline_basis": "MPI mpi_lsbsort 830 M elem/s (64 nodes x 128 cores, n=2^36; BASELINE.md §1)",
         "library": lsbsort.build_info(),

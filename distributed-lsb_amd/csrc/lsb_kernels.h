@@ -192,7 +192,15 @@ hipError_t launch_onesweep(const Elem* in, Elem* out, int64_t m, int shift, int 
 // in -> out.  A segment longer than kSegMax records sets *err (output
 // invalid: the runtime sorts the kept input by the LSD passes instead).
 // grid: persistent workgroups (3 per CU).
-constexpr int kSegMax = 1024;
+// 64: past ~32 records per segment the walks cost more than the LSD passes
+// the hybrid saves (64 per segment: k_segsort 69 ms against 7 for a byte
+// pass), and each walk is bounded by kSegMax each way, so
+// duplicate-heavy keys that do not look skewed (e.g. 2^20 distinct keys,
+// ~1000 copies each, at 2^30 records) cost the hybrid at most a few ms of
+// walks before the sort redoes the kept input by the LSD passes (advisor
+// r03).  Uniform keys at the runtime's k hold ~0.25-2 records per segment
+// (the longest of 2^33 records: ~17).
+constexpr int kSegMax = 64;
 hipError_t launch_segsort(const Elem* in, Elem* out, int64_t m, uint64_t pmask, uint32_t* err,
                           int grid, hipStream_t s);
 // After a SegPass launch in -> out over m records on the byte at `shift`

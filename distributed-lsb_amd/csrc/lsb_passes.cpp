@@ -280,6 +280,9 @@ int sort_hybrid_rank(lsb_ctx* c, Rank& r, int* passes, uint64_t* varying) {
   bool hybrid = msd.size() < digits.size();
   // The first byte sorted on decides the stage split and whether keys are
   // skewed (*skewed: a bucket over 1/32 of the records).
+  // *constant: one bucket holds every record (the byte is constant here; only
+  // possible for the guessed bytes, with LSB_OPT_SKIP_CONSTANT_DIGITS off).
+  bool constant = false;
   auto first_hist = [&](int byte, bool* skewed) -> int {
     if (byte != counted) {
       LSB_TRY(count_byte(c, r, byte, false));
@@ -291,12 +294,20 @@ int sort_hybrid_rank(lsb_ctx* c, Rank& r, int* passes, uint64_t* varying) {
     const int h = lsb::onesweep_halves_for(r.os_hist_h, m);
     r.os_halves = c->os_split == 0 ? h : (c->os_split == 2 ? 2 : 1);
     *skewed = h == 2;
+    constant = false;
+    for (int b = 0; b < lsb::kBuckets && !constant; ++b) {
+      uint64_t tot = 0;
+      for (int x = 0; x < lsb::kOnesweepSubs; ++x) tot += r.os_hist_h[x * lsb::kBuckets + b];
+      constant = tot == (uint64_t)m;
+    }
     return LSB_OK;
   };
   bool skewed = false;
   if (hybrid && !msd.empty()) {
     LSB_TRY(first_hist(msd[0], &skewed));
-    if (skewed) hybrid = false;
+    // Skewed keys make long segments; a constant first byte means the guessed
+    // top bytes are not where the keys vary (advisor r03): the LSD passes.
+    if (skewed || constant) hybrid = false;
   }
   if (!hybrid) {
     if (!digits.empty()) LSB_TRY(first_hist(digits[0], &skewed));

@@ -157,11 +157,12 @@ def test_crossing_runs_past_one_window(lsb_built, oracle_mod, mids, run):
     assert lp == 3  # 3 byte passes, segments merged by k_segfix
 
 
-@pytest.mark.parametrize("bases", [1024, 4096])
+@pytest.mark.parametrize("bases", [1024, 4096, 1 << 15])
 def test_long_segments_fall_back_to_lsd(lsb_built, oracle_mod, bases):
     """n / bases records share each of `bases` random top parts: the first
-    byte looks uniform (no skew), but segments hold ~1024-4096 records, past
-    k_segsort's limit, so the sort redoes the kept input by the LSD passes."""
+    byte looks uniform (no skew), but segments hold ~128-4096 records, past
+    the segment sorts' limit (kSegMax = 64), so the sort redoes the kept input
+    by the LSD passes."""
     rng = np.random.default_rng(bases)
     n = 1 << 22
     top = rng.integers(0, 2**64 - 1, bases, dtype=np.uint64) & np.uint64(0xFFFFFFFFFF000000)
@@ -171,6 +172,17 @@ def test_long_segments_fall_back_to_lsd(lsb_built, oracle_mod, bases):
     out, (lp, _, _), _ = _sort(lsb_built, a)
     assert np.array_equal(out, oracle_mod.stable_sort(a))
     assert lp == 3 + 1 + 8  # 3 byte passes + the failed segment sorts + the LSD passes
+
+
+def test_constant_top_byte_takes_lsd(lsb_built, oracle_mod):
+    """Digit skipping off: the hybrid guesses the top bytes of full 64-bit
+    keys; keys below 2^32 make the first of them constant, and the sort takes
+    the LSD passes at once (8 passes, no segment sort; advisor r03)."""
+    a = _uniform(300_007, 5)
+    a["key"] &= np.uint64(0xFFFFFFFF)
+    out, (lp, _, _), _ = _sort(lsb_built, a, skip=0)
+    assert np.array_equal(out, oracle_mod.stable_sort(a))
+    assert lp == 8
 
 
 def test_generated_input_verifies(lsb_built, digests, oracle_mod):

@@ -40,8 +40,8 @@ def thinned_keys(rng, n):
         elif r < 0.45:  # few values
             pool = g.integers(0, 256, rng.choice((2, 4, 16)), dtype=np.uint64)
             k = (k & ~(np.uint64(0xFF) << sh)) | (pool[g.integers(0, pool.size, n)] << sh)
-    if rng.random() < 0.2:  # duplicates
-        k = k[g.integers(0, max(1, n // rng.choice((2, 8, 64))), n)]
+    if rng.random() < 0.2:  # duplicates: ~2 .. ~1024 copies of each key
+        k = k[g.integers(0, max(1, n // rng.choice((2, 8, 64, 256, 1024))), n)]
     a = np.zeros(n, dtype=DT)
     a["key"] = k
     a["val"] = np.arange(n, dtype=np.uint64)
@@ -70,6 +70,7 @@ def main():
             n = min(n, 1 << 22)
             dist = "thinned"
         desc = f"iter {it}: n={n} P={P} bits={bits} dist={dist} split={split} hybrid={hybrid} gather={gather}"
+        t0 = time.time()
         try:
             with lsbsort.World(n, ranks=P, radix_bits=bits) as w:
                 w.set_option(lsbsort.OPT_ONESWEEP_SPLIT, split)
@@ -92,7 +93,7 @@ def main():
             ok, first, srt = False, str(e), False
         if not (ok and srt):
             bad += 1
-        print(f"{desc} verify={ok} first_bad={first} sorted={srt}", flush=True)
+        print(f"{desc} verify={ok} first_bad={first} sorted={srt} ms={(time.time() - t0) * 1e3:.0f}", flush=True)
         it += 1
     print(f"done: {bad} of {it} sorts wrong", flush=True)
     sys.exit(1 if bad else 0)
