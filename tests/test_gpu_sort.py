@@ -168,6 +168,10 @@ def _masked_keys(n, mask, rng):
     (0x0000000000FFFFFF, 16, 3, 3, 2, 3, 2),        # 16-bit: digits 0,1; byte 3 skipped
     (0xFF00000000000000, 16, 4, 3, 2, 1, 1),        # 16-bit: digit 3's high byte (+ digit 0 forced)
     (0x00000000FFFF0000, 16, 8, 4, 2, 2, 1),        # digit 1 (+ digit 0 forced)
+    # 16-bit: digit 1's low byte constant, so the pass after exchange 0 is
+    # digit 1's high byte, gathered and counting the 65536 digits
+    # (k_onesweep<..., C16, GATHER>)
+    (0x00000000FF00FFFF, 16, 3, 3, 2, 3, 2),
 ])
 @pytest.mark.parametrize("onesweep", [1, 0])
 def test_constant_digits_skipped(lsb_built, oracle_mod, mask, bits, P, passes, exchanges,
