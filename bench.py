@@ -551,6 +551,12 @@ def peer_argv(a):
     return extra_argv(a, ["--exchange", "peer", "--radix-bits", str(a.radix_bits or 16)])
 
 
+def extra_timeout(a):
+    """Seconds an extra form's processes get (a few sorts of the workload):
+    a hung extra costs its keys and this much of the run, not the headline."""
+    return min(a.rank_timeout, 420)
+
+
 def extras_at(a, N):
     """The extra forms timed after the headline, in fresh processes: (name,
     argv).  N > 1: the whole-key exchange and the peer-store exchange (unless
@@ -592,7 +598,7 @@ def rank_extra(a, d, out, name, argv):
     reads its child's line."""
     port = d.bcast_bytes(free_port() if d.rank == 0 else None)
     env = rank_env(d.rank, d.world, d.local_rank, port, os.environ.get("MASTER_ADDR", "127.0.0.1"))
-    ok, text, report = spawn_ranks(argv, [env], a.rank_timeout, f"{name} extra")
+    ok, text, report = spawn_ranks(argv, [env], extra_timeout(a), f"{name} extra")
     ok = d.all_true(ok)
     if d.rank == 0:
         merge_extra(out, name, ok, text, report or ("" if ok else "another rank's process failed"))
@@ -653,7 +659,7 @@ def launch(a):
     for name, xargv in extras_at(a, N):
         port = free_port()
         merge_extra(out, name, *spawn_ranks(xargv, [rank_env(r, N, r, port) for r in range(N)],
-                                            a.rank_timeout, f"{name} extra"))
+                                            extra_timeout(a), f"{name} extra"))
     out["cpu_baseline"] = None if a.no_cpu_baseline else cpu_baseline(out["config"]["n_total"], a.cpu_n)
     print(json.dumps(out), flush=True)
     if out.get("verified") is False or out.get("whole_key_verified") is False:
@@ -896,7 +902,7 @@ def main():
         if N > 1:
             rank_extra(a, d, out, name, xargv)
         else:
-            merge_extra(out, name, *spawn_ranks(xargv, [dict(os.environ)], a.rank_timeout, f"{name} extra"))
+            merge_extra(out, name, *spawn_ranks(xargv, [dict(os.environ)], extra_timeout(a), f"{name} extra"))
     if d.rank == 0 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(n_total, a.cpu_n)
     elif d.rank == 0:
