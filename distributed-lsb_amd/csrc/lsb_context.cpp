@@ -88,10 +88,11 @@ int max_chunks_for_device(int dev) {
 // LSB_PLACEMENT_CANDIDATES (environment, default 4; 2 or less: A and B as
 // allocated), for buffers of at least 1 GiB and only as many as fit in 90 %
 // of the free memory.  Cost at 2^30 records: ~0.2 s at context creation.
-int alloc_records(lsb_ctx* c, Rank& r) {
-  const size_t per = (size_t)c->per;
-  const double bytes = (double)per * sizeof(Elem);
-  int K = 4;
+namespace {
+
+// How many candidate buffers of `bytes` to try (<= 2: no probing).
+int placement_candidates(double bytes, int want) {
+  int K = want;
   if (const char* e = getenv("LSB_PLACEMENT_CANDIDATES")) K = atoi(e);
   K = std::min(K, 8);
   size_t free_b = 0, total_b = 0;
@@ -101,53 +102,75 @@ int alloc_records(lsb_ctx* c, Rank& r) {
     (void)hipGetLastError();
     K = 2;
   }
-  r.placement_k = K > 2 ? K : 0;
-  if (K <= 2) {
-    LSB_TRY(dev_alloc(&r.A, per));
-    return dev_alloc(&r.B, per);
+  return K;
+}
+
+// Times the probe copy x -> y on the rank's stream (best of two, ms).
+struct Prober {
+  hipStream_t s;
+  int64_t m;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  hipError_t err = hipSuccess;
+  Prober(hipStream_t s_, int64_t m_) : s(s_), m(m_) {
+    err = hipEventCreate(&e0);
+    if (err == hipSuccess) err = hipEventCreate(&e1);
   }
-  std::vector<Elem*> cand;
+  ~Prober() {
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+  }
+  double time(const Elem* x, Elem* y) {
+    float best = 1e30f;
+    for (int rep = 0; rep < 2 && err == hipSuccess; ++rep) {
+      err = hipEventRecord(e0, s);
+      if (err == hipSuccess) err = lsb::launch_probe_runs(x, y, m, s);
+      if (err == hipSuccess) err = hipEventRecord(e1, s);
+      if (err == hipSuccess) err = hipEventSynchronize(e1);
+      float t = 0.f;
+      if (err == hipSuccess) err = hipEventElapsedTime(&t, e0, e1);
+      best = std::min(best, t);
+    }
+    return best;
+  }
+};
+
+// Up to K buffers of per records (at least `need`).
+int alloc_candidates(size_t per, int K, size_t need, std::vector<Elem*>& cand) {
+  cand.clear();
   for (int k = 0; k < K; ++k) {
     Elem* p = nullptr;
     if (dev_alloc(&p, per) != LSB_OK) break;  // fewer candidates than hoped
     cand.push_back(p);
   }
   (void)hipGetLastError();
-  auto release = [&](Elem* keep0, Elem* keep1) {
-    for (Elem* p : cand)
-      if (p != keep0 && p != keep1) (void)hipFree(p);
-  };
-  if (cand.size() < 2) {
-    release(nullptr, nullptr);
-    return fail(LSB_ERR_NOMEM, "alloc_records", "record buffers");
+  if (cand.size() >= need) return LSB_OK;
+  for (Elem* p : cand) (void)hipFree(p);
+  cand.clear();
+  return fail(LSB_ERR_NOMEM, "alloc_candidates", "record buffers");
+}
+
+}  // namespace
+
+int alloc_records(lsb_ctx* c, Rank& r) {
+  const size_t per = (size_t)c->per;
+  int K = placement_candidates((double)per * sizeof(Elem), 4);
+  r.placement_k = 0;
+  if (K <= 2) {
+    LSB_TRY(dev_alloc(&r.A, per));
+    return dev_alloc(&r.B, per);
   }
+  std::vector<Elem*> cand;
+  LSB_TRY(alloc_candidates(per, K, 2, cand));
   K = (int)cand.size();
-  r.placement_k = K;
-  hipEvent_t e0 = nullptr, e1 = nullptr;
   std::vector<double> ms((size_t)K * K, 0.0);
-  hipError_t err = hipEventCreate(&e0);
-  if (err == hipSuccess) err = hipEventCreate(&e1);
-  if (err == hipSuccess) err = lsb::launch_probe_runs(cand[0], cand[1], c->per, r.stream);  // warm-up
-  for (int x = 0; x < K && err == hipSuccess; ++x)
-    for (int y = 0; y < K && err == hipSuccess; ++y) {
-      if (x == y) continue;
-      float best = 1e30f;
-      for (int rep = 0; rep < 2 && err == hipSuccess; ++rep) {
-        err = hipEventRecord(e0, r.stream);
-        if (err == hipSuccess) err = lsb::launch_probe_runs(cand[x], cand[y], c->per, r.stream);
-        if (err == hipSuccess) err = hipEventRecord(e1, r.stream);
-        if (err == hipSuccess) err = hipEventSynchronize(e1);
-        float t = 0.f;
-        if (err == hipSuccess) err = hipEventElapsedTime(&t, e0, e1);
-        best = std::min(best, t);
-      }
-      ms[(size_t)x * K + y] = best;
-    }
-  if (e0) (void)hipEventDestroy(e0);
-  if (e1) (void)hipEventDestroy(e1);
-  if (err != hipSuccess) {
-    release(nullptr, nullptr);
-    return fail(LSB_ERR_HIP, "alloc_records: placement probe", hipGetErrorString(err));
+  Prober pr(r.stream, c->per);
+  if (pr.err == hipSuccess) pr.err = lsb::launch_probe_runs(cand[0], cand[1], c->per, r.stream);  // warm-up
+  for (int x = 0; x < K; ++x)
+    for (int y = 0; y < K; ++y)
+      if (x != y) ms[(size_t)x * K + y] = pr.time(cand[x], cand[y]);
+  if (pr.err != hipSuccess) {
+    for (Elem* p : cand) (void)hipFree(p);
+    return fail(LSB_ERR_HIP, "alloc_records: placement probe", hipGetErrorString(pr.err));
   }
   int bx = 0, by = 1;
   double best = 1e300, worst = 0.0;
@@ -161,12 +184,47 @@ int alloc_records(lsb_ctx* c, Rank& r) {
       }
       worst = std::max(worst, pair);
     }
+  r.placement_k = K;
   r.placement_ms[0] = best;
   r.placement_ms[1] = 0.5 * (ms[1] + ms[(size_t)K]);  // the first two buffers allocated
   r.placement_ms[2] = worst;
   r.A = cand[bx];
   r.B = cand[by];
-  release(r.A, r.B);
+  for (Elem* p : cand)
+    if (p != r.A && p != r.B) (void)hipFree(p);
+  return LSB_OK;
+}
+
+// The third record buffer R (receive buffer of the exchanges, the hybrid's
+// third pass buffer), placed like A and B: among up to 3 candidates, the one
+// the probe copies from A and from B write fastest (A and B may hold records
+// by now, so they are only read; the write side is where buffers differ,
+// profiles/r04/allocbw_*.log).
+int alloc_third(lsb_ctx* c, Rank& r) {
+  const size_t per = (size_t)c->per;
+  int K = r.placement_k > 0 ? placement_candidates((double)per * sizeof(Elem), 3) : 1;
+  if (K <= 2) K = 1;
+  if (K == 1) return dev_alloc(&r.R, per);
+  std::vector<Elem*> cand;
+  LSB_TRY(alloc_candidates(per, K, 1, cand));
+  K = (int)cand.size();
+  Prober pr(r.stream, c->per);
+  int bk = 0;
+  double best = 1e300;
+  for (int k = 0; k < K && K > 1; ++k) {
+    const double t = pr.time(r.A, cand[k]) + pr.time(r.B, cand[k]);
+    if (t < best) {
+      best = t;
+      bk = k;
+    }
+  }
+  if (pr.err != hipSuccess) {
+    for (Elem* p : cand) (void)hipFree(p);
+    return fail(LSB_ERR_HIP, "alloc_third: placement probe", hipGetErrorString(pr.err));
+  }
+  r.R = cand[bk];
+  for (Elem* p : cand)
+    if (p != r.R) (void)hipFree(p);
   return LSB_OK;
 }
 

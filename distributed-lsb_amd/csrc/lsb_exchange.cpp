@@ -128,7 +128,7 @@ int place_range(lsb_ctx* c, Rank& r, int shift, int src_rank, const Elem* src, i
 int ensure_recv(lsb_ctx* c, Rank& r) {
   if (r.R) return LSB_OK;
   HIP_TRY(hipSetDevice(r.dev));
-  return dev_alloc(&r.R, (size_t)c->per);
+  return alloc_third(c, r);
 }
 
 // The self segment needs no transfer: place it straight out of A as soon as

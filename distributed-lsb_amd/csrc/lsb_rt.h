@@ -266,6 +266,8 @@ int host_alloc(T** p, size_t count) {
 
 // ---- context and rank buffers (lsb_context.cpp) -------------------------------
 int max_chunks_for_device(int dev);
+int alloc_records(lsb_ctx* c, Rank& r);  // A and B (placement-calibrated)
+int alloc_third(lsb_ctx* c, Rank& r);    // R, placed against A and B
 int init_rank(lsb_ctx* c, Rank& r, int rank, int dev);
 void free_rank(Rank& r);
 Rank* local_rank(lsb_ctx* c, int rank);

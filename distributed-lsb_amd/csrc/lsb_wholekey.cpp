@@ -92,7 +92,7 @@ int merge_owner_counts(int64_t n, int P, int me, const MergeGeom& g, const std::
 
 int merge_ensure(lsb_ctx* c, Rank& r, const MergeGeom& g) {
   HIP_TRY(hipSetDevice(r.dev));
-  if (!r.R) LSB_TRY(dev_alloc(&r.R, (size_t)c->per));
+  if (!r.R) LSB_TRY(ensure_recv(c, r));
   if (!r.merge_path)
     LSB_TRY(dev_alloc(&r.merge_path, (size_t)(lsb::merge_tiles(c->per) + 2 * lsb::kMergeMaxPairs + 1)));
   const int Q = (int)g.target.size();

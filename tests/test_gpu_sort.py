@@ -733,6 +733,17 @@ def test_placement_calibrated_buffers(lsb_built, monkeypatch):
         w.generate()
         w.my_sort()
         assert w.verify() == (True, -1)
+        # the third buffer (hybrid) is placed against A and B by reading them:
+        # the input in A survives its probe
+        w.set_option(lsb_built.OPT_HYBRID, 1)
+        w.generate()
+        w.my_sort()
+        assert w.verify() == (True, -1)
+    with lsb_built.World(n, ranks=1, radix_bits=16) as w:  # R of the exchange path
+        w.set_option(lsb_built.OPT_FORCE_EXCHANGE, 1)
+        w.generate()
+        w.my_sort()
+        assert w.verify() == (True, -1)
     monkeypatch.setenv("LSB_PLACEMENT_CANDIDATES", "2")
     with lsb_built.World(n, ranks=1) as w:
         assert w.placement()["candidates"] == 0
