@@ -33,6 +33,24 @@ def test_exports_every_declared_symbol(lsb_built):
     assert not missing, missing
 
 
+def test_exchange_stats_struct_layout(lsb_built, tmp_path):
+    """lsbsort.ExchangeStats (ctypes) has lsb_exchange_stats_t's layout:
+    every field's offset and the size, as the C compiler lays them out."""
+    import ctypes
+    import subprocess
+    fields = [f for f, _ in lsb_built.ExchangeStats._fields_]
+    src = tmp_path / "layout.c"
+    src.write_text('#include <stddef.h>\n#include <stdio.h>\n#include "lsb.h"\nint main(void) {\n' +
+                   "".join(f'  printf("%zu\\n", offsetof(lsb_exchange_stats_t, {f}));\n' for f in fields) +
+                   '  printf("%zu\\n", sizeof(lsb_exchange_stats_t));\n  return 0;\n}\n')
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.dirname(HEADER), str(src), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
+    want = [getattr(lsb_built.ExchangeStats, f).offset for f in fields] + [ctypes.sizeof(lsb_built.ExchangeStats)]
+    assert got == want
+    assert lsb_built.MAX_RANKS == 64 and len(lsb_built.KERNEL_NAMES) == 9
+
+
 def test_partition_helpers(lsb_built, oracle_mod):
     for n in (0, 1, 2, 7, 20, 1000003, 1 << 33):
         for P in (1, 2, 3, 4, 5, 8, 13):

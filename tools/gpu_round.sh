@@ -85,6 +85,14 @@ for s in $RUN; do
         done
       done
       grep -h verified $O/placement_c*.log ;;
+    allocpmc)  # counters of the placement probe (tools/allocbw_counters.sh)
+      TAG=$TAG/allocpmc SETS="${PMC_SETS:-list tcc utcl}" bash tools/allocbw_counters.sh > $O/allocpmc.log 2>&1 \
+        || fail allocpmc $O/allocpmc.log
+      grep -h "buffer .: read" $O/allocpmc/*.log | head -20 ;;
+    abx)  # gathered passes on / off for the forced 16-bit exchange, uniform and Zipf (tools/ab.sh)
+      TAG=$TAG/abx ROUNDS=${ABX_ROUNDS:-4} FORMS="x16 x16-g0 x16zipf x16zipf-g0" bash tools/ab.sh \
+        cur=distributed-lsb_amd/build/liblsb.so > $O/abx.log 2>&1 || fail abx $O/abx.log
+      tail -20 $O/abx.log ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
