@@ -172,7 +172,11 @@ int alloc_records(lsb_ctx* c, Rank& r) {
     for (Elem* p : cand) (void)hipFree(p);
     return fail(LSB_ERR_HIP, "alloc_records: placement probe", hipGetErrorString(pr.err));
   }
-  int bx = 0, by = 1;
+  // LSB_PLACEMENT_PICK=worst keeps the slowest pair instead (experiments:
+  // tools/alloc_probe.py checks that the probe predicts the passes).
+  const char* pick = getenv("LSB_PLACEMENT_PICK");
+  const bool pick_worst = pick && strcmp(pick, "worst") == 0;
+  int bx = 0, by = 1, wx = 0, wy = 1;
   double best = 1e300, worst = 0.0;
   for (int x = 0; x < K; ++x)
     for (int y = x + 1; y < K; ++y) {
@@ -182,8 +186,17 @@ int alloc_records(lsb_ctx* c, Rank& r) {
         bx = x;
         by = y;
       }
-      worst = std::max(worst, pair);
+      if (pair > worst) {
+        worst = pair;
+        wx = x;
+        wy = y;
+      }
     }
+  if (pick_worst) {
+    std::swap(bx, wx);
+    std::swap(by, wy);
+    std::swap(best, worst);
+  }
   r.placement_k = K;
   r.placement_ms[0] = best;
   r.placement_ms[1] = 0.5 * (ms[1] + ms[(size_t)K]);  // the first two buffers allocated

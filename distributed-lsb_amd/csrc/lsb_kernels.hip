@@ -1152,7 +1152,18 @@ __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_
     auto write_out = [&](auto skew_tag, int h) {
       constexpr bool kSkew = decltype(skew_tag)::value;
       const int jend = HALVES == 1 || (h + 1) * HT >= nvalid ? nvalid : (h + 1) * HT;
+#if LSB_OS_ROTATE
+      // Experiment: each tile starts its write sweep at a pseudo-random stage
+      // position (a multiple of 64) and wraps, so the chip's workgroups do not
+      // sweep the 256 bucket frontiers in step.
+      const int span = jend - h * HT;
+      int rot = SEG ? 0 : (int)((((uint32_t)tile * 2654435761u) >> 16) % (uint32_t)(span > 0 ? span : 1)) & ~63;
+      for (int k = t; k < span; k += BLOCK) {
+        int j = h * HT + k + rot;
+        if (j >= jend) j -= span;
+#else
       for (int j = h * HT + t; j < jend; j += BLOCK) {
+#endif
         const Elem v = stage[j - h * HT];
         const uint32_t d = (uint32_t)(v.key >> shift) & (kBuckets - 1);
         int pos = j;
@@ -1720,18 +1731,24 @@ __global__ __launch_bounds__(256) void k_check_sorted(const Elem* __restrict__ A
   }
 }
 
-// Buffer-placement probe (launch_probe_runs): record i = (tile t, slot j)
-// of `in` goes to bucket b = j / 16 of `out`, at b * (m / 256) + t * 16 +
-// j % 16: every 4096-record tile sends one 256-byte run to each of 256 bucket
-// frontiers, the write pattern of an LSD pass, with sequential reads.
+// Buffer-placement probe (launch_probe_runs): the traffic of one LSD pass
+// without its sort.  The records are cut like k_onesweep's: 8 sub-arrays of
+// 4096-record tiles, read tile by tile in each sub-array, the 8 advancing
+// together (virtual tile g is tile g / 8 of sub-array g % 8); slot j of a tile
+// goes to bucket j / 16 at the sub-array's part of the bucket's range, so
+// every tile sends a 256-byte run to each of 256 buckets and 2048 write
+// frontiers advance together, as in a pass over uniform keys.
 __global__ __launch_bounds__(256) void k_probe_runs(const Elem* __restrict__ in, Elem* __restrict__ out,
                                                     int64_t m) {
-  const int64_t per_bucket = m / kBuckets;
-  const int64_t n = per_bucket * kBuckets;
+  const int64_t n = m & ~(int64_t)((kTile * kSub) - 1);  // whole tiles in every sub-array
+  const int64_t sub = n / kSub, part = n / (kSub * kBuckets), bucket = n / kBuckets;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    const int64_t t = i >> 12;
+    const int64_t g = i >> 12;
     const int j = (int)(i & (kTile - 1));
-    store_elem(out + (int64_t)(j >> 4) * per_bucket + t * 16 + (j & 15), load_elem_nt(in + i));
+    const int x = (int)(g & (kSub - 1));
+    const int64_t tl = g >> 3;
+    store_elem(out + (int64_t)(j >> 4) * bucket + x * part + tl * 16 + (j & 15),
+               load_elem_nt(in + x * sub + tl * kTile + j));
   }
 }
 
@@ -2044,7 +2061,7 @@ hipError_t launch_verify(const Elem* A, int64_t here, int64_t gbase, int64_t n, 
 }
 
 hipError_t launch_probe_runs(const Elem* in, Elem* out, int64_t m, hipStream_t s) {
-  if (m < (int64_t)kTile * kBuckets) return hipErrorInvalidValue;  // >= 16 records per run and bucket
+  if (m < (int64_t)kTile * kSub) return hipErrorInvalidValue;  // a tile in every sub-array
   hipLaunchKernelGGL(k_probe_runs, dim3(8192), dim3(256), 0, s, in, out, m);
   return hipGetLastError();
 }

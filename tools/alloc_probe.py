@@ -30,8 +30,13 @@ lg = int(sys.argv[1]) if len(sys.argv) > 1 else 30
 ctxs = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 reps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
 n = 1 << lg
+# LSB_PICKS="best,worst,...": the placement pick of each context in turn
+# (LSB_PLACEMENT_PICK: does the probe's choice predict the pass times?)
+picks = [p for p in os.environ.get("LSB_PICKS", "").split(",") if p]
 worlds = []
 for c in range(ctxs):
+    if picks:
+        os.environ["LSB_PLACEMENT_PICK"] = picks[c % len(picks)]
     w = lsbsort.World(n, ranks=1, radix_bits=8)
     worlds.append(w)
     w.generate()
@@ -51,6 +56,7 @@ for c in range(ctxs):
         print(json.dumps({"context": c, "rep": r, "ms": round(ms, 2), "passes": passes}), flush=True)
     ok, _ = w.verify()
     print(json.dumps({"context": c, "verified": ok, "placement": w.placement(),
+                      "pick": os.environ.get("LSB_PLACEMENT_PICK", "best"),
                       "env_candidates": os.environ.get("LSB_PLACEMENT_CANDIDATES", "default")}), flush=True)
 for w in worlds:
     w.close()

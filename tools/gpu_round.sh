@@ -93,6 +93,16 @@ for s in $RUN; do
       TAG=$TAG/abx ROUNDS=${ABX_ROUNDS:-4} FORMS="x16 x16-g0 x16zipf x16zipf-g0" bash tools/ab.sh \
         cur=distributed-lsb_amd/build/liblsb.so > $O/abx.log 2>&1 || fail abx $O/abx.log
       tail -20 $O/abx.log ;;
+    pick)  # does the placement probe predict k_onesweep? best / worst pair alternately, 2 processes
+      for k in 1 2; do
+        LSB_PICKS=best,worst,best,worst timeout -k 10 300 python -u tools/alloc_probe.py 30 4 2 \
+          >> $O/pick.log 2>&1 || fail pick $O/pick.log
+      done
+      grep -h verified $O/pick.log ;;
+    rot)  # A/B: rotated write sweep (-DLSB_OS_ROTATE=1, abtest/rot) against the tree's build
+      TAG=$TAG/rot ROUNDS=${ROT_ROUNDS:-4} FORMS="uniform zipf" bash tools/ab.sh \
+        base=distributed-lsb_amd/build/liblsb.so rot=abtest/rot/liblsb.so > $O/rot.log 2>&1 || fail rot $O/rot.log
+      tail -12 $O/rot.log ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
