@@ -151,27 +151,64 @@ int alloc_candidates(size_t per, int K, size_t need, std::vector<Elem*>& cand) {
 
 }  // namespace
 
+// Times one k_onesweep pass x -> y over the rank's here records on the byte
+// at `shift`, with the rank's own look-back rows and histograms
+// (onesweep_ensure); the histogram read before it is not timed.
+double time_pass(Rank& r, Prober& pr, const Elem* x, Elem* y, int shift) {
+  if (pr.err != hipSuccess) return 0.0;
+  pr.err = lsb::launch_subhist(x, r.here, shift, r.os_grid, r.os_hist, nullptr, r.stream);
+  uint32_t epoch = r.os_epoch + 1;
+  if (epoch >= (1u << 30)) epoch = 2;  // as onesweep_launch: keep the parity alternation
+  if (pr.err == hipSuccess) pr.err = hipEventRecord(pr.e0, r.stream);
+  if (pr.err == hipSuccess)
+    pr.err = lsb::launch_onesweep(x, y, r.here, shift, -1, r.os_hist, nullptr, r.os_status, r.os_ctr, epoch,
+                                  r.os_ctr + lsb::kOnesweepSubs, r.os_grid, r.stream);
+  if (pr.err == hipSuccess) r.os_epoch = epoch;
+  if (pr.err == hipSuccess) pr.err = hipEventRecord(pr.e1, r.stream);
+  if (pr.err == hipSuccess) pr.err = hipEventSynchronize(pr.e1);
+  float t = 0.f;
+  if (pr.err == hipSuccess) pr.err = hipEventElapsedTime(&t, pr.e0, pr.e1);
+  return t;
+}
+
+// A and B.  The probe is the pass itself: each candidate gets uniform PCG
+// keys, and one k_onesweep pass is timed between every ordered pair (on a
+// byte the source is not ordered by).  A copy with the same write pattern
+// (launch_probe_runs) ranked the buffers by their streaming write speed, but
+// that did not predict the pass, whose tile loads sit on its look-back chain
+// (profiles/r04/placement_*.log, pick.log).
 int alloc_records(lsb_ctx* c, Rank& r) {
   const size_t per = (size_t)c->per;
   int K = placement_candidates((double)per * sizeof(Elem), 4);
   r.placement_k = 0;
-  if (K <= 2) {
+  if (K <= 2 || r.here < (int64_t)lsb::kTile * lsb::kOnesweepSubs || r.here > lsb::kOnesweepMaxElems) {
     LSB_TRY(dev_alloc(&r.A, per));
     return dev_alloc(&r.B, per);
   }
   std::vector<Elem*> cand;
   LSB_TRY(alloc_candidates(per, K, 2, cand));
   K = (int)cand.size();
-  std::vector<double> ms((size_t)K * K, 0.0);
-  Prober pr(r.stream, c->per);
-  if (pr.err == hipSuccess) pr.err = lsb::launch_probe_runs(cand[0], cand[1], c->per, r.stream);  // warm-up
-  for (int x = 0; x < K; ++x)
-    for (int y = 0; y < K; ++y)
-      if (x != y) ms[(size_t)x * K + y] = pr.time(cand[x], cand[y]);
-  if (pr.err != hipSuccess) {
+  auto give_up = [&](int rc) {
     for (Elem* p : cand) (void)hipFree(p);
-    return fail(LSB_ERR_HIP, "alloc_records: placement probe", hipGetErrorString(pr.err));
-  }
+    return rc;
+  };
+  int rc = onesweep_ensure(r);
+  if (rc != LSB_OK) return give_up(rc);
+  std::vector<double> ms((size_t)K * K, 0.0);
+  std::vector<int> sorted_by(K, -8);
+  Prober pr(r.stream, r.here);
+  for (int k = 0; k < K && pr.err == hipSuccess; ++k)
+    pr.err = lsb::launch_pcg_fill(cand[k], r.here, 0x5eed + (uint64_t)k, 0, lsb::KeyGen(), r.stream);
+  (void)time_pass(r, pr, cand[0], cand[1], 0);  // warm-up
+  sorted_by[1] = 0;
+  for (int x = 0; x < K; ++x)
+    for (int y = 0; y < K; ++y) {
+      if (x == y) continue;
+      const int shift = (sorted_by[x] + 8) & 63;
+      ms[(size_t)x * K + y] = time_pass(r, pr, cand[x], cand[y], shift);
+      sorted_by[y] = shift;
+    }
+  if (pr.err != hipSuccess) return give_up(fail(LSB_ERR_HIP, "alloc_records: placement probe", hipGetErrorString(pr.err)));
   // LSB_PLACEMENT_PICK=worst keeps the slowest pair instead (experiments:
   // tools/alloc_probe.py checks that the probe predicts the passes).
   const char* pick = getenv("LSB_PLACEMENT_PICK");
