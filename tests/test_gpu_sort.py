@@ -744,6 +744,14 @@ def test_placement_calibrated_buffers(lsb_built, monkeypatch):
         w.generate()
         w.my_sort()
         assert w.verify() == (True, -1)
+    monkeypatch.setenv("LSB_PLACEMENT_PICK", "worst")  # the experiment hook keeps the slowest pair
+    with lsb_built.World(n, ranks=1) as w:
+        p = w.placement()
+        assert p["candidates"] == 4 and p["chosen_ms"] == p["worst_ms"] >= p["first_pair_ms"], p
+        w.generate()
+        w.my_sort()
+        assert w.verify() == (True, -1)
+    monkeypatch.delenv("LSB_PLACEMENT_PICK")
     monkeypatch.setenv("LSB_PLACEMENT_CANDIDATES", "2")
     with lsb_built.World(n, ranks=1) as w:
         assert w.placement()["candidates"] == 0
