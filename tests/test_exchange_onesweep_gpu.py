@@ -203,3 +203,24 @@ def test_gathered_pass_matches_placed(lsb_built, oracle_mod, n, P, bits):
     assert np.array_equal(outs[0], outs[1])
     assert stats[0]["place"][0] == stats[1]["place"][0]
     assert stats[0]["upsweep"][0] == stats[1]["upsweep"][0] == P  # one k_subhist per rank
+
+
+@pytest.mark.parametrize("split", [0, 2])
+def test_skewed_keys_gather(lsb_built, oracle_mod, split):
+    """Zipf keys pick the split stage (auto, 0) or have it forced (2); their
+    exchanges still only count the arriving records but the last, and the
+    gathered passes take the whole stage (round 4):
+    lsb_get_exchange_stats shows every record counted at 3 of the 4
+    exchanges and placed at the last."""
+    P, n = 2, 200_003
+    a = _dist("zipf", n, np.random.default_rng(17 + split))
+    with lsb_built.World(n, ranks=P, radix_bits=16) as w:
+        w.set_option(lsb_built.OPT_ONESWEEP_SPLIT, split)
+        w.scatter_global(a)
+        w.reset_kernel_stats()
+        w.my_sort()
+        assert np.array_equal(w.gather_global(), oracle_mod.stable_sort(a))
+        ex = w.last_sort()[1]
+        x = w.exchange_stats()
+        assert ex >= 2 and x["exchanges"] == ex
+        assert x["placed_records"] == n and x["counted_records"] == n * (ex - 1), x
