@@ -230,12 +230,11 @@ int alloc_records(lsb_ctx* c, Rank& r) {
       }
     }
   if (pick_worst) {
-    std::swap(bx, wx);
-    std::swap(by, wy);
-    std::swap(best, worst);
+    bx = wx;
+    by = wy;
   }
   r.placement_k = K;
-  r.placement_ms[0] = best;
+  r.placement_ms[0] = pick_worst ? worst : best;
   r.placement_ms[1] = 0.5 * (ms[1] + ms[(size_t)K]);  // the first two buffers allocated
   r.placement_ms[2] = worst;
   r.A = cand[bx];
