@@ -109,6 +109,14 @@ for s in $RUN; do
         python3 $R/bench.py --steps 8 --warmup 2 --no-cpu-baseline --no-traffic --no-extras) > $O/clock.log 2>&1 \
         || fail clock $O/clock.log
       python3 tools/clock_summary.py $O/clock | tail -20 ;;
+    kcand)  # the bench's case: the FIRST context of fresh processes, 4 vs 8 placement candidates
+      for k in 1 2 3 4; do
+        for cand in 4 8; do
+          LSB_PLACEMENT_CANDIDATES=$cand timeout -k 10 200 python -u tools/alloc_probe.py 30 1 3 \
+            >> $O/kcand_c$cand.log 2>&1 || fail kcand $O/kcand_c$cand.log
+        done
+      done
+      python3 tools/pick_summary.py $O/kcand_c4.log $O/kcand_c8.log ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
