@@ -75,19 +75,18 @@ int max_chunks_for_device(int dev) {
 
 // ---- record buffers A and B, placement-calibrated ----------------------------
 // How fast an LSD pass streams between two 16 GiB record buffers depends on
-// where the driver placed them.  tools/kbench/allocbw.hip, four fresh
-// processes of four 2^30-record buffers each (profiles/r04/allocbw_*.log):
-// pure streaming reads are level (2.85-3.0 ms), but the LSD write pattern
-// (256 bucket frontiers, 256-byte runs) copies X -> Y in 5.7-5.9 ms into some
-// buffers, 6.85-6.9 ms into most, and 7.2-7.3 ms between some pairs, in both
-// directions -- the same +-5 % that k_onesweep's pass times showed from
-// context to context (tools/alloc_probe.py, profiles/ab/r03_alloc_*).  So a
-// rank's A and B are chosen among K candidate buffers: each ordered pair is
-// timed with that copy (launch_probe_runs), the pair with the smallest sum of
-// both directions (the passes ping-pong) is kept, the rest are freed.  K =
-// LSB_PLACEMENT_CANDIDATES (environment, default 4; 2 or less: A and B as
-// allocated), for buffers of at least 1 GiB and only as many as fit in 90 %
-// of the free memory.  Cost at 2^30 records: ~0.2 s at context creation.
+// where the driver placed them: per buffer the write side runs
+// at 5.6-6.9 TB/s (tools/kbench/allocbw.hip, profiles/r04/allocbw_*.log), and
+// k_onesweep's passes at 6.7-7.3 ms between pairs allocated in one process
+// (profiles/r04/v5_pick.log).  So a rank's A and B are chosen among K
+// candidate buffers by timing one k_onesweep pass between every ordered pair;
+// the pair with the smallest sum of both directions (the passes ping-pong) is
+// kept and the rest are freed.  K = LSB_PLACEMENT_CANDIDATES (environment,
+// default 8; 2 or less: A and B as allocated), for buffers of at least 1 GiB
+// and only as many as fit in 90 % of the free memory.  Eight candidates found
+// a pair at 6.71-6.72 ms in each of four fresh processes, where four found one
+// only in two of four (profiles/r04/v6_kcand_c{4,8}.log).  Cost at 2^30
+// records: ~0.7 s at context creation, 128 GiB held while it runs.
 namespace {
 
 // How many candidate buffers of `bytes` to try (<= 2: no probing).
@@ -179,7 +178,7 @@ double time_pass(Rank& r, Prober& pr, const Elem* x, Elem* y, int shift) {
 // (profiles/r04/placement_*.log, pick.log).
 int alloc_records(lsb_ctx* c, Rank& r) {
   const size_t per = (size_t)c->per;
-  int K = placement_candidates((double)per * sizeof(Elem), 4);
+  int K = placement_candidates((double)per * sizeof(Elem), 8);
   r.placement_k = 0;
   if (K <= 2 || r.here < (int64_t)lsb::kTile * lsb::kOnesweepSubs || r.here > lsb::kOnesweepMaxElems) {
     LSB_TRY(dev_alloc(&r.A, per));

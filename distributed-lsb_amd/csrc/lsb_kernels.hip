@@ -1152,18 +1152,7 @@ __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_
     auto write_out = [&](auto skew_tag, int h) {
       constexpr bool kSkew = decltype(skew_tag)::value;
       const int jend = HALVES == 1 || (h + 1) * HT >= nvalid ? nvalid : (h + 1) * HT;
-#if LSB_OS_ROTATE
-      // Experiment: each tile starts its write sweep at a pseudo-random stage
-      // position (a multiple of 64) and wraps, so the chip's workgroups do not
-      // sweep the 256 bucket frontiers in step.
-      const int span = jend - h * HT;
-      int rot = SEG ? 0 : (int)((((uint32_t)tile * 2654435761u) >> 16) % (uint32_t)(span > 0 ? span : 1)) & ~63;
-      for (int k = t; k < span; k += BLOCK) {
-        int j = h * HT + k + rot;
-        if (j >= jend) j -= span;
-#else
       for (int j = h * HT + t; j < jend; j += BLOCK) {
-#endif
         const Elem v = stage[j - h * HT];
         const uint32_t d = (uint32_t)(v.key >> shift) & (kBuckets - 1);
         int pos = j;

@@ -302,13 +302,13 @@ int  lsb_get_pass_exchange(lsb_ctx_t* ctx, int pass, int64_t* bytes, double* wir
 
 /* How the local rank's record buffers A and B were placed: at creation a rank
  * whose buffers hold >= 1 GiB allocates `candidates` buffers (environment
- * LSB_PLACEMENT_CANDIDATES, default 4; 0 here: A and B as allocated), times a
- * copy with an LSD pass's write pattern (256 bucket frontiers of 256-byte
- * runs) between every ordered pair, keeps the pair fastest both ways and
- * frees the rest (the speed of that copy varies by up to ~25 % with where the
- * driver puts a 16 GiB buffer).  Milliseconds per copy, mean of
- * both directions: the chosen pair, the first two buffers allocated (what a
- * plain allocation would have kept) and the slowest pair. */
+ * LSB_PLACEMENT_CANDIDATES, default 8, as many as fit; 0 here: A and B as
+ * allocated), times one k_onesweep pass over uniform keys between every
+ * ordered pair, keeps the pair fastest both ways and frees the rest (the pass
+ * runs up to ~8 % slower between some pairs than others, with where the driver
+ * puts a 16 GiB buffer).  Milliseconds per pass, mean of both
+ * directions: the chosen pair, the first two buffers allocated (what a plain
+ * allocation would have kept) and the slowest pair. */
 int  lsb_get_placement(lsb_ctx_t* ctx, int rank, int* candidates, double* chosen_ms,
                        double* first_pair_ms, double* worst_ms);
 

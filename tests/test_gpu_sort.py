@@ -721,14 +721,14 @@ def test_harness_rccl_ranks_share_gpu(lsb_built, ref_vectors, n, P, extra):
 
 # ------------------------------------------ placement-calibrated A and B
 def test_placement_calibrated_buffers(lsb_built, monkeypatch):
-    """A rank whose record buffers hold >= 1 GiB picks A and B among 4
-    candidate buffers by a probe copy (lsb_get_placement); with
+    """A rank whose record buffers hold >= 1 GiB picks A and B among 8
+    candidate buffers by a timed pass (lsb_get_placement); with
     LSB_PLACEMENT_CANDIDATES=2 it keeps the first two allocated.  Either way
     the sort is the same (verified on device)."""
     n = 1 << 26  # 1 GiB per buffer
     with lsb_built.World(n, ranks=1) as w:
         p = w.placement()
-        assert p["candidates"] == 4, p
+        assert p["candidates"] == 8, p
         assert 0 < p["chosen_ms"] <= p["first_pair_ms"] <= p["worst_ms"], p
         w.generate()
         w.my_sort()
@@ -747,7 +747,7 @@ def test_placement_calibrated_buffers(lsb_built, monkeypatch):
     monkeypatch.setenv("LSB_PLACEMENT_PICK", "worst")  # the experiment hook keeps the slowest pair
     with lsb_built.World(n, ranks=1) as w:
         p = w.placement()
-        assert p["candidates"] == 4 and p["chosen_ms"] == p["worst_ms"] >= p["first_pair_ms"], p
+        assert p["candidates"] == 8 and p["chosen_ms"] == p["worst_ms"] >= p["first_pair_ms"], p
         w.generate()
         w.my_sort()
         assert w.verify() == (True, -1)

@@ -10,8 +10,8 @@ ones.
 
     python tools/alloc_probe.py [LG] [CONTEXTS] [REPS]
 
-LSB_PLACEMENT_CANDIDATES=2 allocates A and B as they come; the default (4)
-picks them among 4 candidates by a probe copy (lsb_get_placement).
+LSB_PLACEMENT_CANDIDATES=2 allocates A and B as they come; the default (8)
+picks them among 8 candidates by a timed pass (lsb_get_placement).
 
 (A build whose record buffers came from hipExtMallocWithFlags(...,
 hipDeviceMallocContiguous) ran every pass ~48 % slower, 10.3-10.9 ms:
