@@ -275,7 +275,10 @@ def measure_traffic(a, kernel, elems):
                 for f in files:
                     if f.endswith("counter_collection.csv"):
                         for r in csv.DictReader(open(os.path.join(root, f))):
-                            if r["Counter_Name"] == counter and kernel in r["Kernel_Name"]:
+                            name = r["Kernel_Name"]
+                            # the placement probe's passes at context creation
+                            # run as k_onesweep_probe: not the sort's launches
+                            if r["Counter_Name"] == counter and kernel in name and "_probe" not in name:
                                 per[r.get("Dispatch_Id", len(per))].append(float(r["Counter_Value"]))
             if not per:
                 return None, f"no {counter} rows for {kernel}"
@@ -890,8 +893,9 @@ def main():
         "exchange_bytes_per_step": xbytes // a.steps if N > 1 else 0,
         "exchange_roofline": xroof,
         "placement": dict(placement, basis="rank 0's A and B, chosen at context creation among `candidates` "
-                                            "buffers by an LSD-pattern probe copy, ms per copy (lsb_get_placement; "
-                                            "DESIGN.md 4)"),
+                                            "buffers by one timed k_onesweep pass between every ordered pair; ms "
+                                            "per pass, mean of both directions: the kept pair, the first two "
+                                            "allocated, the slowest (lsb_get_placement; DESIGN.md 4)"),
         "verified": verified,
         "vs_baseline_basis": "MPI mpi_lsbsort 830 M elem/s (64 nodes x 128 cores, n=2^36; BASELINE.md §1)",
         "library": lsbsort.build_info(),

@@ -159,9 +159,11 @@ double time_pass(Rank& r, Prober& pr, const Elem* x, Elem* y, int shift) {
   uint32_t epoch = r.os_epoch + 1;
   if (epoch >= (1u << 30)) epoch = 2;  // as onesweep_launch: keep the parity alternation
   if (pr.err == hipSuccess) pr.err = hipEventRecord(pr.e0, r.stream);
+  lsb::OnesweepExtra probe;
+  probe.probe = true;  // k_onesweep_probe: the same pass under its own name (profiles)
   if (pr.err == hipSuccess)
     pr.err = lsb::launch_onesweep(x, y, r.here, shift, -1, r.os_hist, nullptr, r.os_status, r.os_ctr, epoch,
-                                  r.os_ctr + lsb::kOnesweepSubs, r.os_grid, r.stream);
+                                  r.os_ctr + lsb::kOnesweepSubs, r.os_grid, r.stream, probe);
   if (pr.err == hipSuccess) r.os_epoch = epoch;
   if (pr.err == hipSuccess) pr.err = hipEventRecord(pr.e1, r.stream);
   if (pr.err == hipSuccess) pr.err = hipEventSynchronize(pr.e1);

@@ -176,6 +176,7 @@ struct OnesweepExtra {
   int halves = 1;  // 2: split stage, 3 workgroups per CU (skewed keys; not with count16)
   const SegPass* seg = nullptr;  // the hybrid's last pass (no next digit, whole stage)
   const GatherSrc* gather = nullptr;  // records gathered from an exchange (`in` unused)
+  bool probe = false;  // the placement probe's pass (a last pass, launched as k_onesweep_probe)
 };
 // The runtime's choice of OnesweepExtra::halves for a rank, from a digit's
 // sub-array histogram (kOnesweepSubs x 256 counts of m records): 2 when one
