@@ -104,7 +104,7 @@ int placement_candidates(double bytes, int want) {
   return K;
 }
 
-// Times the probe copy x -> y on the rank's stream (best of two, ms).
+// Events of the placement probe on the rank's stream.
 struct Prober {
   hipStream_t s;
   int64_t m;
@@ -117,19 +117,6 @@ struct Prober {
   ~Prober() {
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
-  }
-  double time(const Elem* x, Elem* y) {
-    float best = 1e30f;
-    for (int rep = 0; rep < 2 && err == hipSuccess; ++rep) {
-      err = hipEventRecord(e0, s);
-      if (err == hipSuccess) err = lsb::launch_probe_runs(x, y, m, s);
-      if (err == hipSuccess) err = hipEventRecord(e1, s);
-      if (err == hipSuccess) err = hipEventSynchronize(e1);
-      float t = 0.f;
-      if (err == hipSuccess) err = hipEventElapsedTime(&t, e0, e1);
-      best = std::min(best, t);
-    }
-    return best;
   }
 };
 
@@ -153,16 +140,18 @@ int alloc_candidates(size_t per, int K, size_t need, std::vector<Elem*>& cand) {
 // Times one k_onesweep pass x -> y over the rank's here records on the byte
 // at `shift`, with the rank's own look-back rows and histograms
 // (onesweep_ensure); the histogram read before it is not timed.
-double time_pass(Rank& r, Prober& pr, const Elem* x, Elem* y, int shift) {
+// hist: kOnesweepSubs * 256 u32 of scratch (r.os_hist at creation; a buffer
+// of its own once a sort may hold a histogram in r.os_hist).
+double time_pass(Rank& r, Prober& pr, const Elem* x, Elem* y, int shift, uint32_t* hist) {
   if (pr.err != hipSuccess) return 0.0;
-  pr.err = lsb::launch_subhist(x, r.here, shift, r.os_grid, r.os_hist, nullptr, r.stream);
+  pr.err = lsb::launch_subhist(x, r.here, shift, r.os_grid, hist, nullptr, r.stream);
   uint32_t epoch = r.os_epoch + 1;
   if (epoch >= (1u << 30)) epoch = 2;  // as onesweep_launch: keep the parity alternation
   if (pr.err == hipSuccess) pr.err = hipEventRecord(pr.e0, r.stream);
   lsb::OnesweepExtra probe;
   probe.probe = true;  // k_onesweep_probe: the same pass under its own name (profiles)
   if (pr.err == hipSuccess)
-    pr.err = lsb::launch_onesweep(x, y, r.here, shift, -1, r.os_hist, nullptr, r.os_status, r.os_ctr, epoch,
+    pr.err = lsb::launch_onesweep(x, y, r.here, shift, -1, hist, nullptr, r.os_status, r.os_ctr, epoch,
                                   r.os_ctr + lsb::kOnesweepSubs, r.os_grid, r.stream, probe);
   if (pr.err == hipSuccess) r.os_epoch = epoch;
   if (pr.err == hipSuccess) pr.err = hipEventRecord(pr.e1, r.stream);
@@ -175,7 +164,7 @@ double time_pass(Rank& r, Prober& pr, const Elem* x, Elem* y, int shift) {
 // A and B.  The probe is the pass itself: each candidate gets uniform PCG
 // keys, and one k_onesweep pass is timed between every ordered pair (on a
 // byte the source is not ordered by).  A copy with the same write pattern
-// (launch_probe_runs) ranked the buffers by their streaming write speed, but
+// (tools/kbench/allocbw.hip) ranked the buffers by their streaming write speed, but
 // that did not predict the pass, whose tile loads sit on its look-back chain
 // (profiles/r04/placement_*.log, pick.log).
 int alloc_records(lsb_ctx* c, Rank& r) {
@@ -200,13 +189,13 @@ int alloc_records(lsb_ctx* c, Rank& r) {
   Prober pr(r.stream, r.here);
   for (int k = 0; k < K && pr.err == hipSuccess; ++k)
     pr.err = lsb::launch_pcg_fill(cand[k], r.here, 0x5eed + (uint64_t)k, 0, lsb::KeyGen(), r.stream);
-  (void)time_pass(r, pr, cand[0], cand[1], 0);  // warm-up
+  (void)time_pass(r, pr, cand[0], cand[1], 0, r.os_hist);  // warm-up
   sorted_by[1] = 0;
   for (int x = 0; x < K; ++x)
     for (int y = 0; y < K; ++y) {
       if (x == y) continue;
       const int shift = (sorted_by[x] + 8) & 63;
-      ms[(size_t)x * K + y] = time_pass(r, pr, cand[x], cand[y], shift);
+      ms[(size_t)x * K + y] = time_pass(r, pr, cand[x], cand[y], shift, r.os_hist);
       sorted_by[y] = shift;
     }
   if (pr.err != hipSuccess) return give_up(fail(LSB_ERR_HIP, "alloc_records: placement probe", hipGetErrorString(pr.err)));
@@ -247,30 +236,37 @@ int alloc_records(lsb_ctx* c, Rank& r) {
 
 // The third record buffer R (receive buffer of the exchanges, the hybrid's
 // third pass buffer), placed like A and B: among up to 3 candidates, the one
-// the probe copies from A and from B write fastest (A and B may hold records
-// by now, so they are only read; the write side is where buffers differ,
-// profiles/r04/allocbw_*.log).
+// whose timed passes to and from B (scratch whenever R is first needed:
+// before a hybrid sort, at an exchange before its placement) take least time.
+// A may hold records by then and is not touched; the probe counts into a
+// histogram of its own, since a sort may hold one in r.os_hist.
 int alloc_third(lsb_ctx* c, Rank& r) {
   const size_t per = (size_t)c->per;
   int K = r.placement_k > 0 ? placement_candidates((double)per * sizeof(Elem), 3) : 1;
   if (K <= 2) K = 1;
-  if (K == 1) return dev_alloc(&r.R, per);
+  if (K == 1 || !r.os_status) return dev_alloc(&r.R, per);
   std::vector<Elem*> cand;
   LSB_TRY(alloc_candidates(per, K, 1, cand));
   K = (int)cand.size();
-  Prober pr(r.stream, c->per);
+  uint32_t* hist = nullptr;
+  int rc = K > 1 ? dev_alloc(&hist, (size_t)lsb::kOnesweepSubs * lsb::kBuckets) : LSB_OK;
+  Prober pr(r.stream, r.here);
   int bk = 0;
   double best = 1e300;
-  for (int k = 0; k < K && K > 1; ++k) {
-    const double t = pr.time(r.A, cand[k]) + pr.time(r.B, cand[k]);
+  for (int k = 0; k < K && K > 1 && rc == LSB_OK; ++k) {
+    if (pr.err == hipSuccess)
+      pr.err = lsb::launch_pcg_fill(cand[k], r.here, 0x5eed + 16 + (uint64_t)k, 0, lsb::KeyGen(), r.stream);
+    const double t = time_pass(r, pr, cand[k], r.B, 0, hist) + time_pass(r, pr, r.B, cand[k], 8, hist);
     if (t < best) {
       best = t;
       bk = k;
     }
   }
-  if (pr.err != hipSuccess) {
+  (void)hipFree(hist);
+  if (rc == LSB_OK && pr.err != hipSuccess) rc = fail(LSB_ERR_HIP, "alloc_third: placement probe", hipGetErrorString(pr.err));
+  if (rc != LSB_OK) {
     for (Elem* p : cand) (void)hipFree(p);
-    return fail(LSB_ERR_HIP, "alloc_third: placement probe", hipGetErrorString(pr.err));
+    return rc;
   }
   r.R = cand[bk];
   for (Elem* p : cand)

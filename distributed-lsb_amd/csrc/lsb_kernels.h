@@ -289,12 +289,6 @@ hipError_t launch_merge_level(const MergeLevel& level, int64_t* path, int grid, 
 hipError_t launch_verify(const Elem* A, int64_t here, int64_t gbase, int64_t n, int64_t per,
                          KeyGen gen, unsigned long long* first_bad, hipStream_t s);
 
-// Buffer-placement probe: out <- in (m records) with an LSD pass's traffic
-// (k_onesweep's 8 sub-arrays of 4096-record tiles read in order, 256-byte
-// runs to 256 buckets x 8 sub-array parts).  The runtime times it between
-// candidate record buffers (lsb_context.cpp).
-hipError_t launch_probe_runs(const Elem* in, Elem* out, int64_t m, hipStream_t s);
-
 // Key-only local sortedness (checkSorted); *unsorted set to 1 on a descent.
 hipError_t launch_check_sorted(const Elem* A, int64_t here, unsigned int* unsorted, hipStream_t s);
 

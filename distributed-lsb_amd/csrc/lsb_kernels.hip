@@ -1746,27 +1746,6 @@ __global__ __launch_bounds__(256) void k_check_sorted(const Elem* __restrict__ A
   }
 }
 
-// Buffer-placement probe (launch_probe_runs): the traffic of one LSD pass
-// without its sort.  The records are cut like k_onesweep's: 8 sub-arrays of
-// 4096-record tiles, read tile by tile in each sub-array, the 8 advancing
-// together (virtual tile g is tile g / 8 of sub-array g % 8); slot j of a tile
-// goes to bucket j / 16 at the sub-array's part of the bucket's range, so
-// every tile sends a 256-byte run to each of 256 buckets and 2048 write
-// frontiers advance together, as in a pass over uniform keys.
-__global__ __launch_bounds__(256) void k_probe_runs(const Elem* __restrict__ in, Elem* __restrict__ out,
-                                                    int64_t m) {
-  const int64_t n = m & ~(int64_t)((kTile * kSub) - 1);  // whole tiles in every sub-array
-  const int64_t sub = n / kSub, part = n / (kSub * kBuckets), bucket = n / kBuckets;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    const int64_t g = i >> 12;
-    const int j = (int)(i & (kTile - 1));
-    const int x = (int)(g & (kSub - 1));
-    const int64_t tl = g >> 3;
-    store_elem(out + (int64_t)(j >> 4) * bucket + x * part + tl * 16 + (j & 15),
-               load_elem_nt(in + x * sub + tl * kTile + j));
-  }
-}
-
 int grid_for(int64_t work, int block, int cap) {
   const int64_t g = (work + block - 1) / block;
   return (int)(g < 1 ? 1 : (g > cap ? cap : g));
@@ -2077,12 +2056,6 @@ hipError_t launch_verify(const Elem* A, int64_t here, int64_t gbase, int64_t n, 
   if (here <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_verify, dim3(grid_for(here, 256, 8192)), dim3(256), 0, s, A, here, gbase, n,
                      per, gen, first_bad);
-  return hipGetLastError();
-}
-
-hipError_t launch_probe_runs(const Elem* in, Elem* out, int64_t m, hipStream_t s) {
-  if (m < (int64_t)kTile * kSub) return hipErrorInvalidValue;  // a tile in every sub-array
-  hipLaunchKernelGGL(k_probe_runs, dim3(8192), dim3(256), 0, s, in, out, m);
   return hipGetLastError();
 }
 
