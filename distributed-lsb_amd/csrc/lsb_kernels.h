@@ -1,5 +1,5 @@
-// Internal interface between the runtime (lsb_runtime.cpp) and the HIP
-// kernels (lsb_kernels.hip).  Not part of the C ABI (that is include/lsb.h).
+// Internal interface between the runtime (lsb_context.cpp, lsb_passes.cpp,
+// lsb_exchange.cpp, lsb_wholekey.cpp) and the HIP kernels (lsb_kernels.hip).  Not part of the C ABI (that is include/lsb.h).
 #pragma once
 
 #include <hip/hip_runtime.h>

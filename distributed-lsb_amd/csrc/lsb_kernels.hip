@@ -1147,14 +1147,79 @@ __device__ __forceinline__ void onesweep_body(
 #endif
     if (t == 0) grab(nxt_tile, nxt_sub);  // in flight during the writes
 
-    // The loop is instantiated twice (the launch-uniform `skewed` picks one
-    // outside it): a per-record branch on it cost uniform keys 2.4 %.
-    auto write_out = [&](auto skew_tag, int h) {
+    // emit: one staged record (tile position j, output slot delta + pos) to
+    // memory, and its next digit to the sub-array histogram.
+    // g = delta[digit] + the record's slot in its run, c = cut[digit].
+    auto emit = [&](auto skew_tag, const Elem& v, int j, int64_t g, uint32_t c) {
       constexpr bool kSkew = decltype(skew_tag)::value;
+      LSB_DASSERT(g >= 0 && g < m);
+      // In range by construction.  The clamp keeps a look-back that gave up
+      // (err set, output reported invalid) from storing outside `out`; a
+      // clamp, not a branch: the conditional store cost 6 % of the sort.
+      const uint64_t gs = (uint64_t)g < (uint64_t)(m - 1) ? (uint64_t)g : (uint64_t)(m - 1);
+      store_elem(out + gs, v);
+      if (NEXT) {
+        const uint32_t xs = (uint32_t)j >= (c & 0xFFFFu) ? (c >> 24) : ((c >> 16) & 0xFFu);
+        const uint32_t dn = (uint32_t)(v.key >> next_shift) & (kBuckets - 1);
+        const uint32_t slot = xs * kBuckets + dn;
+        if (kSkew) {
+          // One add per run of equal slots within the wave-instruction: the
+          // head lane of each run adds the run's length.  Hot keys come in
+          // long runs in the staged (bucket-ordered) tile, so the 64-way
+          // same-address LDS atomics that serialise become one or two adds.
+          // Active lanes are a prefix (j < nvalid), so a run ends at the
+          // next head or at the active count.
+          // The previous lane's slot by DPP wave_shr:1 (lane 0 keeps ~slot,
+          // so it is always a head); __shfl_up is a ds_bpermute round trip
+          // (-1.5 % Zipf, uniform unchanged: profiles/ab/r02_ab7_*).
+          const uint64_t act = __ballot(1);
+          const uint32_t prev =
+              (uint32_t)__builtin_amdgcn_update_dpp((int)~slot, (int)slot, 0x138, 0xf, 0xf, false);
+          const bool head = prev != slot;
+          const uint64_t heads = __ballot(head);
+          if (head) {
+            const uint64_t above = heads & ~((2ull << lane) - 1ull);
+            const uint32_t end = above ? (uint32_t)__builtin_ctzll(above) : (uint32_t)__popcll(act);
+            atomicAdd(&nh[slot], end - lane);
+          }
+        } else {
+          atomicAdd(&nh[slot], 1u);
+        }
+      }
+    };
+    // The write-out is instantiated twice (the launch-uniform `skewed` picks
+    // one outside it): a per-record branch on it cost uniform keys 2.4 %.
+    auto write_out = [&](auto skew_tag, int h) {
       const int jend = HALVES == 1 || (h + 1) * HT >= nvalid ? nvalid : (h + 1) * HT;
+      // A whole tile: every thread's T / BLOCK records read from the stage
+      // together, then their delta and cut entries, so the LDS round trips
+      // overlap instead of serialising twice per record (-0.6...-0.9 % per
+      // sort, profiles/r04/ab_wo/).  Only the LSD passes' whole-stage
+      // instances: the exchange's and the split stage's would spill.
+      if (!SEG && HALVES == 1 && !C16 && !GATHER && jend == HT) {
+        constexpr int G = HT / BLOCK;
+        {
+          Elem v[G];
+          int64_t dl[G];
+          uint32_t ct[G];
+#pragma unroll
+          for (int k = 0; k < G; ++k) v[k] = stage[k * BLOCK + t];
+#pragma unroll
+          for (int k = 0; k < G; ++k) {
+            const uint32_t d = (uint32_t)(v[k].key >> shift) & (kBuckets - 1);
+            dl[k] = delta[d];
+            ct[k] = NEXT ? cut[d] : 0u;
+          }
+#pragma unroll
+          for (int k = 0; k < G; ++k) {
+            const int j = k * BLOCK + t;
+            emit(skew_tag, v[k], j, dl[k] + j, ct[k]);
+          }
+        }
+        return;
+      }
       for (int j = h * HT + t; j < jend; j += BLOCK) {
         const Elem v = stage[j - h * HT];
-        const uint32_t d = (uint32_t)(v.key >> shift) & (kBuckets - 1);
         int pos = j;
         if (SEG) {
           // Stage neighbours j - 1 and j + 1 are the neighbouring lanes'
@@ -1197,42 +1262,8 @@ __device__ __forceinline__ void onesweep_body(
             pos = sfirst + (int)(less + eqb);
           }
         }
-        const int64_t g = delta[d] + pos;
-        LSB_DASSERT(g >= 0 && g < m);
-        // In range by construction.  The clamp keeps a look-back that gave up
-        // (err set, output reported invalid) from storing outside `out`; a
-        // clamp, not a branch: the conditional store cost 6 % of the sort.
-        const uint64_t gs = (uint64_t)g < (uint64_t)(m - 1) ? (uint64_t)g : (uint64_t)(m - 1);
-        store_elem(out + gs, v);
-        if (NEXT) {
-          const uint32_t c = cut[d];
-          const uint32_t xs = (uint32_t)j >= (c & 0xFFFFu) ? (c >> 24) : ((c >> 16) & 0xFFu);
-          const uint32_t dn = (uint32_t)(v.key >> next_shift) & (kBuckets - 1);
-          const uint32_t slot = xs * kBuckets + dn;
-          if (kSkew) {
-            // One add per run of equal slots within the wave-instruction: the
-            // head lane of each run adds the run's length.  Hot keys come in
-            // long runs in the staged (bucket-ordered) tile, so the 64-way
-            // same-address LDS atomics that serialise become one or two adds.
-            // Active lanes are a prefix (j < nvalid), so a run ends at the
-            // next head or at the active count.
-            // The previous lane's slot by DPP wave_shr:1 (lane 0 keeps ~slot,
-            // so it is always a head); __shfl_up is a ds_bpermute round trip
-            // (-1.5 % Zipf, uniform unchanged: profiles/ab/r02_ab7_*).
-            const uint64_t act = __ballot(1);
-            const uint32_t prev =
-                (uint32_t)__builtin_amdgcn_update_dpp((int)~slot, (int)slot, 0x138, 0xf, 0xf, false);
-            const bool head = prev != slot;
-            const uint64_t heads = __ballot(head);
-            if (head) {
-              const uint64_t above = heads & ~((2ull << lane) - 1ull);
-              const uint32_t end = above ? (uint32_t)__builtin_ctzll(above) : (uint32_t)__popcll(act);
-              atomicAdd(&nh[slot], end - lane);
-            }
-          } else {
-            atomicAdd(&nh[slot], 1u);
-          }
-        }
+        const uint32_t d = (uint32_t)(v.key >> shift) & (kBuckets - 1);
+        emit(skew_tag, v, j, delta[d] + pos, NEXT ? cut[d] : 0u);
       }
     };
     for (int h = 0; h < HALVES; ++h) {

@@ -10,6 +10,8 @@
 //     bytes, segments ordered by k_segfix / k_segsort (lsb_segsort.hip).
 #include "lsb_rt.h"
 
+#include <deque>
+
 namespace lsb_rt {
 
 // ---- one local stable 8-bit pass A -> B, then swap (localShuffle) -------
@@ -183,58 +185,38 @@ int onesweep_digits(lsb_ctx* c, Rank& r, const std::vector<int>& digits, int* pa
   return LSB_OK;
 }
 
-int sort_hybrid_rank(lsb_ctx* c, Rank& r, int* passes, uint64_t* varying);
-
-// lsb_sort when nothing is exchanged: one k_subhist read (digit 0's
+// ---- a rank's local sort, in three steps -----------------------------------
+// LocalSort is one rank's local sort as begin() (queue the first count read
+// and its read-backs), queue() (wait for those, queue the passes) and
+// finish() (the hybrid: read its error word; rarely, sort again).
+// sort_local_rank runs the steps back to back; sort_local_ranks runs each step
+// on every rank before the next one, so that the host's waits for one rank
+// (the span, the first histogram, the hybrid's error word) do not hold back
+// the other devices of a loopback context (advisor r03).  Each rank keeps
+// its own pass cursor (begin_pass) from step to step.
+//
+// Single-read passes (nothing exchanged): one k_subhist read (digit 0's
 // sub-array histogram and the key span), then one k_onesweep per digit that
 // varies, each also counting the next such digit over its output.  Same
 // output as the reduce-then-scan loop (do_pass).  A constant digit 0 is
 // skipped like any other: its pass would be the identity, so the first
 // digit that varies is counted by a second k_subhist read (a read, not a
 // pass), and that digit's histogram also decides the stage split.
-// Rank r alone (its local block); *passes gets the passes it ran, *varying the
-// key bits that vary in the block.  LSB_OPT_HYBRID: sort_hybrid_rank.
-int sort_onesweep_rank(lsb_ctx* c, Rank& r, int* passes, uint64_t* varying) {
-  if (c->hybrid) return sort_hybrid_rank(c, r, passes, varying);
-  HIP_TRY(hipSetDevice(r.dev));
-  LSB_TRY(onesweep_ensure(r));
-  c->pass_cursor = 0;
-  c->cur_pass = 0;  // the count reads are filed under the first pass
-  HIP_TRY(hipMemsetAsync(r.span, 0, 2 * sizeof(uint64_t), r.stream));
-  LSB_TRY(count_byte(c, r, 0, c->skip_constant));
-  LSB_TRY(queue_halves(c, r, r.os_hist));
-  *varying = ~0ull;
-  *passes = 0;
-  if (c->skip_constant) {
-    HIP_TRY(hipMemcpyAsync(r.span_h, r.span, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, r.stream));
-    HIP_TRY(hipStreamSynchronize(r.stream));
-    *varying = r.span_h[0] & r.span_h[1];
-  }
-  const std::vector<int> digits = varying_bytes(*varying);
-  if (!digits.empty() && digits[0] != 0) {
-    LSB_TRY(count_byte(c, r, digits[0], false));
-    LSB_TRY(queue_halves(c, r, r.os_hist));
-    LSB_TRY(choose_halves(c, r, false));
-  } else {
-    LSB_TRY(choose_halves(c, r, c->skip_constant));
-  }
-  LSB_TRY(onesweep_digits(c, r, digits, passes));
-  // The look-back's give-up word, read by lsb_sync.
-  HIP_TRY(hipMemcpyAsync(r.os_err_h, r.os_ctr + lsb::kOnesweepSubs, sizeof(uint32_t),
-                         hipMemcpyDeviceToHost, r.stream));
-  return LSB_OK;
-}
-
-// ---- hybrid local sort (LSB_OPT_HYBRID) ------------------------------------
-// The same stable order as the LSD passes from fewer passes over HBM
-// (lsb_segsort.hip): k_onesweep passes on the k most significant varying
-// bytes only, then k_segsort orders every segment (run of records equal on
-// those bytes) by the whole key.  k: the fewest top varying bytes whose
-// varying bits reach ceil(log2 m), so uniform keys leave segments of about
-// one record (2^30 records: k = 4, 0.25 on average; k_segsort's walk then
-// costs ~2 LDS reads per record and the pass streams at copy speed.  k = 3,
-// 64 per segment, made k_segsort compute-bound: 69 ms against 7 for the
-// fourth byte's pass, profiles/r03_h1_probe.log).
+//
+// The hybrid (LSB_OPT_HYBRID): the same stable order as the LSD passes from
+// fewer passes over HBM (lsb_segsort.hip): k_onesweep passes on the k most
+// significant varying bytes only, then k_segsort orders every segment (run
+// of records equal on those bytes) by the whole key.  k: the fewest top
+// varying bytes whose varying bits reach ceil(log2 m), so uniform keys leave
+// segments of about one record (2^30 records: k = 4, 0.25 on average;
+// k_segsort's walk then costs ~2 LDS reads per record and the pass streams
+// at copy speed.  k = 3, 64 per segment, made k_segsort compute-bound: 69 ms
+// against 7 for the fourth byte's pass, profiles/r03_h1_probe.log).  The k
+// passes leave the input A untouched (A -> B, then B <-> R), so when
+// k_segsort meets a segment longer than kSegMax the sort starts over from A
+// with the LSD passes; skewed keys (the first pass's byte has a bucket over
+// 1/32 of the records, as for the stage split: duplicate-heavy keys make
+// long segments) take them directly.
 std::vector<int> hybrid_bytes(uint64_t varying, int64_t m) {
   int need = 0;
   while ((int64_t(1) << need) < m) ++need;
@@ -249,213 +231,320 @@ std::vector<int> hybrid_bytes(uint64_t varying, int64_t m) {
   return top;
 }
 
-// The hybrid for rank r.  The k passes leave the input A untouched (A -> B,
-// then B <-> R), so when k_segsort meets a segment longer than kSegMax the
-// sort starts over from A with the LSD passes; skewed keys (the first
-// pass's byte has a bucket over 1/32 of the records, as for the stage
-// split: duplicate-heavy keys make long segments) take them directly.  One
-// host sync, after k_segsort, reads its error word.
-int sort_hybrid_rank(lsb_ctx* c, Rank& r, int* passes, uint64_t* varying) {
-  HIP_TRY(hipSetDevice(r.dev));
-  LSB_TRY(onesweep_ensure(r));
-  LSB_TRY(ensure_recv(c, r));
-  c->pass_cursor = 0;
-  c->cur_pass = 0;
-  const int64_t m = r.here;
-  *passes = 0;
-  *varying = ~0ull;
-  // Count the byte the first pass most likely sorts on (full 64-bit keys)
-  // in the same read as the span.
-  const std::vector<int> guess = hybrid_bytes(~0ull, m);
-  int counted = guess.empty() ? 0 : guess[0];
+namespace {
+
+struct LocalSort {
+  lsb_ctx* c;
+  Rank& r;
+  int passes = 0;        // local passes run
+  uint64_t varying = 0;  // key bits that vary in the block
+  enum Kind { kDone, kLsd, kHybrid } kind = kDone;
+  int cursor = 0, cur = 0;  // this rank's pass cursor between the steps
+  int counted = -1;         // the byte os_hist[0] counts
+  bool hist_queued = false;  // its read-back into os_hist_h is queued
+  std::vector<int> digits, msd;
+  bool fuse = false;
+  // {A, B, R} stays a permutation of {X0, X1, X2} at every step (the pass
+  // loop swaps A and B; R holds X0, the kept input, from the first pass on).
+  // While armed, an error return restores A = X0, B = X1, R = X2, so the
+  // context keeps its input in A and three distinct buffers (advisor r03).
+  Elem *X0 = nullptr, *X1 = nullptr, *X2 = nullptr;
+  bool armed = false;
+  uint64_t pmask = 0;
+  lsb::SegPass sp;
+  const Elem* seg_in = nullptr;  // the last pass's input, read by k_segfix
+  uint32_t* err = nullptr;       // the segment sorts' error word
+
+  LocalSort(lsb_ctx* c_, Rank& r_) : c(c_), r(r_) {}
+  LocalSort(const LocalSort&) = delete;
+  ~LocalSort() {
+    if (armed) {
+      r.A = X0;
+      r.B = X1;
+      r.R = X2;
+    }
+  }
+  struct Step {  // resume and save the rank's pass cursor
+    LocalSort& s;
+    explicit Step(LocalSort& s_) : s(s_) {
+      s.c->pass_cursor = s.cursor;
+      s.c->cur_pass = s.cur;
+    }
+    ~Step() {
+      s.cursor = s.c->pass_cursor;
+      s.cur = s.c->cur_pass;
+    }
+  };
+
+  int begin();
+  int queue();
+  int finish();
+  int classic();
+  int first_hist(int byte, bool* skewed, bool* constant);
+  int queue_err_word() {
+    // The look-back's give-up word, read by lsb_sync.
+    HIP_TRY(hipMemcpyAsync(r.os_err_h, r.os_ctr + lsb::kOnesweepSubs, sizeof(uint32_t),
+                           hipMemcpyDeviceToHost, r.stream));
+    return LSB_OK;
+  }
+};
+
+// Count + scan + scatter passes (the single-read ones do not apply), run whole.
+int LocalSort::classic() {
   HIP_TRY(hipMemsetAsync(r.span, 0, 2 * sizeof(uint64_t), r.stream));
-  LSB_TRY(count_byte(c, r, counted, c->skip_constant));
+  c->pass_cursor = 0;
+  begin_pass(c, 0);
+  LSB_TRY(local_pass(c, r, 0, c->skip_constant));
+  passes = 1;
+  varying = ~0ull;
   if (c->skip_constant) {
     HIP_TRY(hipMemcpyAsync(r.span_h, r.span, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, r.stream));
     HIP_TRY(hipStreamSynchronize(r.stream));
-    *varying = r.span_h[0] & r.span_h[1];
+    varying = r.span_h[0] & r.span_h[1];
   }
-  const std::vector<int> digits = varying_bytes(*varying);
-  const std::vector<int> msd = c->skip_constant ? hybrid_bytes(*varying, m) : guess;
-  bool hybrid = msd.size() < digits.size();
-  // The first byte sorted on decides the stage split and whether keys are
-  // skewed (*skewed: a bucket over 1/32 of the records).
-  // *constant: one bucket holds every record (the byte is constant here; only
-  // possible for the guessed bytes, with LSB_OPT_SKIP_CONSTANT_DIGITS off).
-  bool constant = false;
-  auto first_hist = [&](int byte, bool* skewed) -> int {
-    if (byte != counted) {
-      LSB_TRY(count_byte(c, r, byte, false));
-      counted = byte;
-    }
+  for (int d = 1; d < 64 / lsb::kDigitBits; ++d) {
+    if (((varying >> (d * lsb::kDigitBits)) & (lsb::kBuckets - 1)) == 0) continue;
+    begin_pass(c, d * lsb::kDigitBits);
+    LSB_TRY(local_pass(c, r, d * lsb::kDigitBits));
+    ++passes;
+  }
+  return LSB_OK;
+}
+
+int LocalSort::begin() {
+  Step step(*this);
+  kind = kDone;
+  if (r.here == 0) return LSB_OK;
+  HIP_TRY(hipSetDevice(r.dev));
+  if (!c->onesweep || r.here > lsb::kOnesweepMaxElems) return classic();
+  LSB_TRY(onesweep_ensure(r));
+  c->pass_cursor = 0;
+  c->cur_pass = 0;  // the count reads are filed under the first pass
+  varying = ~0ull;
+  HIP_TRY(hipMemsetAsync(r.span, 0, 2 * sizeof(uint64_t), r.stream));
+  if (c->hybrid) {
+    kind = kHybrid;
+    LSB_TRY(ensure_recv(c, r));
+    // Count the byte the first pass most likely sorts on (full 64-bit keys)
+    // in the same read as the span, and queue its read-back beside the span's.
+    const std::vector<int> guess = hybrid_bytes(~0ull, r.here);
+    counted = guess.empty() ? 0 : guess[0];
+    LSB_TRY(count_byte(c, r, counted, c->skip_constant));
     HIP_TRY(hipMemcpyAsync(r.os_hist_h, r.os_hist, sizeof(uint32_t) * lsb::kOnesweepSubs * lsb::kBuckets,
                            hipMemcpyDeviceToHost, r.stream));
+    hist_queued = true;
+  } else {
+    kind = kLsd;
+    LSB_TRY(count_byte(c, r, 0, c->skip_constant));
+    LSB_TRY(queue_halves(c, r, r.os_hist));
+  }
+  if (c->skip_constant)
+    HIP_TRY(hipMemcpyAsync(r.span_h, r.span, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, r.stream));
+  return LSB_OK;
+}
+
+// The first byte sorted on decides the stage split and whether keys are
+// skewed (*skewed: a bucket over 1/32 of the records).  *constant: one bucket
+// holds every record (the byte is constant here; only possible for the
+// guessed bytes, with LSB_OPT_SKIP_CONSTANT_DIGITS off).
+int LocalSort::first_hist(int byte, bool* skewed, bool* constant) {
+  if (byte != counted) {
+    LSB_TRY(count_byte(c, r, byte, false));
+    counted = byte;
+    hist_queued = false;
+  }
+  if (!hist_queued)
+    HIP_TRY(hipMemcpyAsync(r.os_hist_h, r.os_hist, sizeof(uint32_t) * lsb::kOnesweepSubs * lsb::kBuckets,
+                           hipMemcpyDeviceToHost, r.stream));
+  hist_queued = false;  // the passes overwrite os_hist
+  HIP_TRY(hipStreamSynchronize(r.stream));
+  const int64_t m = r.here;
+  const int h = lsb::onesweep_halves_for(r.os_hist_h, m);
+  r.os_halves = c->os_split == 0 ? h : (c->os_split == 2 ? 2 : 1);
+  *skewed = h == 2;
+  *constant = false;
+  for (int b = 0; b < lsb::kBuckets && !*constant; ++b) {
+    uint64_t tot = 0;
+    for (int x = 0; x < lsb::kOnesweepSubs; ++x) tot += r.os_hist_h[x * lsb::kBuckets + b];
+    *constant = tot == (uint64_t)m;
+  }
+  return LSB_OK;
+}
+
+int LocalSort::queue() {
+  if (kind == kDone) return LSB_OK;
+  Step step(*this);
+  HIP_TRY(hipSetDevice(r.dev));
+  const int64_t m = r.here;
+  if (c->skip_constant) {
     HIP_TRY(hipStreamSynchronize(r.stream));
-    const int h = lsb::onesweep_halves_for(r.os_hist_h, m);
-    r.os_halves = c->os_split == 0 ? h : (c->os_split == 2 ? 2 : 1);
-    *skewed = h == 2;
-    constant = false;
-    for (int b = 0; b < lsb::kBuckets && !constant; ++b) {
-      uint64_t tot = 0;
-      for (int x = 0; x < lsb::kOnesweepSubs; ++x) tot += r.os_hist_h[x * lsb::kBuckets + b];
-      constant = tot == (uint64_t)m;
+    varying = r.span_h[0] & r.span_h[1];
+  }
+  digits = varying_bytes(varying);
+  if (kind == kLsd) {
+    if (!digits.empty() && digits[0] != 0) {
+      LSB_TRY(count_byte(c, r, digits[0], false));
+      LSB_TRY(queue_halves(c, r, r.os_hist));
+      LSB_TRY(choose_halves(c, r, false));
+    } else {
+      LSB_TRY(choose_halves(c, r, c->skip_constant));
     }
-    return LSB_OK;
-  };
-  bool skewed = false;
+    LSB_TRY(onesweep_digits(c, r, digits, &passes));
+    kind = kDone;
+    return queue_err_word();
+  }
+  msd = hybrid_bytes(c->skip_constant ? varying : ~0ull, m);
+  bool hybrid = msd.size() < digits.size();
+  bool skewed = false, constant = false;
   if (hybrid && !msd.empty()) {
-    LSB_TRY(first_hist(msd[0], &skewed));
+    LSB_TRY(first_hist(msd[0], &skewed, &constant));
     // Skewed keys make long segments; a constant first byte means the guessed
     // top bytes are not where the keys vary (advisor r03): the LSD passes.
     if (skewed || constant) hybrid = false;
   }
   if (!hybrid) {
-    if (!digits.empty()) LSB_TRY(first_hist(digits[0], &skewed));
-    LSB_TRY(onesweep_digits(c, r, digits, passes));
-  } else {
-    // The k passes: A -> B, then B <-> R; the input X0 is kept.  The last
-    // one also orders every segment inside its tile (SegPass) and k_segfix
-    // merges the segments split between tiles; LSB_OPT_HYBRID = 2, or the
-    // split stage, leaves the segments to a k_segsort pass instead.
-    Elem* const X0 = r.A;
-    Elem* const X1 = r.B;
-    Elem* const X2 = r.R;
-    // {A, B, R} stays a permutation of {X0, X1, X2} at every step (the pass
-    // loop swaps A and B; R holds X0, the kept input, from the first pass on).
-    // A return on an error restores A = X0, B = X1, R = X2, so the context
-    // keeps its input in A and three distinct buffers (advisor r03).
-    struct Restore {
-      Rank& r;
-      Elem *x0, *x1, *x2;
-      bool armed = true;
-      ~Restore() {
-        if (armed) {
-          r.A = x0;
-          r.B = x1;
-          r.R = x2;
-        }
-      }
-    } restore{r, X0, X1, X2};
-    uint64_t pmask = 0;
-    for (int b : msd) pmask |= (uint64_t)(lsb::kBuckets - 1) << (b * lsb::kDigitBits);
-    uint32_t* err = r.os_ctr + lsb::kOnesweepSubs + 1;
-    const bool fuse = c->hybrid == 1 && r.os_halves == 1 && !msd.empty();
-    lsb::SegPass sp;
-    if (fuse) {
-      if (!r.seg_base) LSB_TRY(dev_alloc(&r.seg_base, (size_t)lsb::kOnesweepSubs * lsb::kBuckets));
-      sp.pmask = pmask;
-      sp.rmask = pmask & ~((uint64_t)(lsb::kBuckets - 1) << (msd.back() * lsb::kDigitBits));
-      sp.base = r.seg_base;
-      sp.err = err;
+    if (!digits.empty()) LSB_TRY(first_hist(digits[0], &skewed, &constant));
+    LSB_TRY(onesweep_digits(c, r, digits, &passes));
+    kind = kDone;
+    return queue_err_word();
+  }
+  // The k passes: A -> B, then B <-> R; the input X0 is kept.  The last one
+  // also orders every segment inside its tile (SegPass) and k_segfix merges
+  // the segments split between tiles; LSB_OPT_HYBRID = 2, or the split stage,
+  // leaves the segments to a k_segsort pass instead.
+  X0 = r.A;
+  X1 = r.B;
+  X2 = r.R;
+  armed = true;
+  for (int b : msd) pmask |= (uint64_t)(lsb::kBuckets - 1) << (b * lsb::kDigitBits);
+  err = r.os_ctr + lsb::kOnesweepSubs + 1;
+  fuse = c->hybrid == 1 && r.os_halves == 1 && !msd.empty();
+  if (fuse) {
+    if (!r.seg_base) LSB_TRY(dev_alloc(&r.seg_base, (size_t)lsb::kOnesweepSubs * lsb::kBuckets));
+    sp.pmask = pmask;
+    sp.rmask = pmask & ~((uint64_t)(lsb::kBuckets - 1) << (msd.back() * lsb::kDigitBits));
+    sp.base = r.seg_base;
+    sp.err = err;
+  }
+  HIP_TRY(hipMemsetAsync(err, 0, sizeof(uint32_t), r.stream));
+  uint32_t* hist[2] = {r.os_hist, r.os_hist + lsb::kOnesweepSubs * lsb::kBuckets};
+  for (size_t i = 0; i < msd.size(); ++i) {
+    const int shift = msd[i] * lsb::kDigitBits;
+    const int next = i + 1 < msd.size() ? msd[i + 1] * lsb::kDigitBits : -1;
+    begin_pass(c, shift);
+    lsb::OnesweepExtra x;
+    x.halves = r.os_halves;
+    if (fuse && i + 1 == msd.size()) {
+      x.seg = &sp;
+      seg_in = r.A;
     }
-    HIP_TRY(hipMemsetAsync(err, 0, sizeof(uint32_t), r.stream));
-    uint32_t* hist[2] = {r.os_hist, r.os_hist + lsb::kOnesweepSubs * lsb::kBuckets};
-    const Elem* seg_in = nullptr;  // the last pass's input, read by k_segfix
-    for (size_t i = 0; i < msd.size(); ++i) {
-      const int shift = msd[i] * lsb::kDigitBits;
-      const int next = i + 1 < msd.size() ? msd[i + 1] * lsb::kDigitBits : -1;
-      begin_pass(c, shift);
-      lsb::OnesweepExtra x;
-      x.halves = r.os_halves;
-      if (fuse && i + 1 == msd.size()) {
-        x.seg = &sp;
-        seg_in = r.A;
-      }
-      LSB_TRY(onesweep_launch(c, r, shift, next, hist[i & 1], hist[(i + 1) & 1], x));
-      ++*passes;
-      if (i == 0) {  // A is X1 now, B is X0: keep X0, write X2 next
-        r.B = X2;
-        r.R = X0;
-      }
-    }
-    if (msd.empty()) {
-      r.B = X1;
-      r.R = X2;
-    }
-    auto sync_err = [&](uint32_t* v) -> int {
-      HIP_TRY(hipMemcpyAsync(r.os_err_h + 1, err, sizeof(uint32_t), hipMemcpyDeviceToHost, r.stream));
-      HIP_TRY(hipStreamSynchronize(r.stream));
-      *v = r.os_err_h[1];
-      return LSB_OK;
-    };
-    bool sorted = false;
-    if (fuse) {
-      {
-        Timer t(c, &r, LSB_K_SEGSORT);
-        // one wave per tile boundary, 32 waves per CU
-        HIP_TRY(lsb::launch_segfix(seg_in, r.A, m, msd.back() * lsb::kDigitBits, r.os_status, sp,
-                                   16 * r.os_grid, r.stream));
-      }
-      uint32_t e = 0;
-      LSB_TRY(sync_err(&e));
-      sorted = e == 0;
-    }
-    if (!sorted) {
-      // k_segsort: r.A is stably sorted by pmask (the fused pass's segments
-      // too, in or out of order).
-      HIP_TRY(hipMemsetAsync(err, 0, sizeof(uint32_t), r.stream));
-      begin_pass(c, 64);
-      {
-        Timer t(c, &r, LSB_K_SEGSORT);
-        HIP_TRY(lsb::launch_segsort(r.A, r.B, m, pmask, err, 3 * r.os_grid / 2, r.stream));
-      }
-      count_pass_elems(c, m, false);
-      ++*passes;
-      uint32_t e = 0;
-      LSB_TRY(sync_err(&e));
-      if (e == 0) {
-        std::swap(r.A, r.B);
-        sorted = true;
-      }
-    }
-    if (sorted) {
-      r.R = (X0 != r.A && X0 != r.B) ? X0 : (X1 != r.A && X1 != r.B) ? X1 : X2;
-      restore.armed = false;
-    } else {  // a segment too long for the segment sorts: the LSD passes over the kept input
-      r.A = X0;
-      r.B = X1;
-      r.R = X2;
-      restore.armed = false;
-      counted = -1;
-      if (!digits.empty()) LSB_TRY(first_hist(digits[0], &skewed));
-      LSB_TRY(onesweep_digits(c, r, digits, passes));
+    LSB_TRY(onesweep_launch(c, r, shift, next, hist[i & 1], hist[(i + 1) & 1], x));
+    ++passes;
+    if (i == 0) {  // A is X1 now, B is X0: keep X0, write X2 next
+      r.B = X2;
+      r.R = X0;
     }
   }
-  // The look-back's give-up word, read by lsb_sync.
-  HIP_TRY(hipMemcpyAsync(r.os_err_h, r.os_ctr + lsb::kOnesweepSubs, sizeof(uint32_t),
-                         hipMemcpyDeviceToHost, r.stream));
+  if (msd.empty()) {
+    r.B = X1;
+    r.R = X2;
+  }
+  if (fuse) {
+    {
+      Timer t(c, &r, LSB_K_SEGSORT);
+      // one wave per tile boundary, 32 waves per CU
+      HIP_TRY(lsb::launch_segfix(seg_in, r.A, m, msd.back() * lsb::kDigitBits, r.os_status, sp,
+                                 16 * r.os_grid, r.stream));
+    }
+    HIP_TRY(hipMemcpyAsync(r.os_err_h + 1, err, sizeof(uint32_t), hipMemcpyDeviceToHost, r.stream));
+  }
+  return LSB_OK;
+}
+
+int LocalSort::finish() {
+  if (kind != kHybrid) return LSB_OK;
+  Step step(*this);
+  HIP_TRY(hipSetDevice(r.dev));
+  auto sync_err = [&](uint32_t* v) -> int {
+    HIP_TRY(hipStreamSynchronize(r.stream));
+    *v = r.os_err_h[1];
+    return LSB_OK;
+  };
+  bool sorted = false;
+  if (fuse) {  // its error word's read-back was queued after k_segfix
+    uint32_t e = 0;
+    LSB_TRY(sync_err(&e));
+    sorted = e == 0;
+  }
+  if (!sorted) {
+    // k_segsort: r.A is stably sorted by pmask (the fused pass's segments
+    // too, in or out of order).
+    HIP_TRY(hipMemsetAsync(err, 0, sizeof(uint32_t), r.stream));
+    begin_pass(c, 64);
+    {
+      Timer t(c, &r, LSB_K_SEGSORT);
+      HIP_TRY(lsb::launch_segsort(r.A, r.B, r.here, pmask, err, 3 * r.os_grid / 2, r.stream));
+    }
+    count_pass_elems(c, r.here, false);
+    ++passes;
+    HIP_TRY(hipMemcpyAsync(r.os_err_h + 1, err, sizeof(uint32_t), hipMemcpyDeviceToHost, r.stream));
+    uint32_t e = 0;
+    LSB_TRY(sync_err(&e));
+    if (e == 0) {
+      std::swap(r.A, r.B);
+      sorted = true;
+    }
+  }
+  kind = kDone;
+  if (sorted) {
+    r.R = (X0 != r.A && X0 != r.B) ? X0 : (X1 != r.A && X1 != r.B) ? X1 : X2;
+    armed = false;
+  } else {  // a segment too long for the segment sorts: the LSD passes over the kept input
+    r.A = X0;
+    r.B = X1;
+    r.R = X2;
+    armed = false;
+    counted = -1;
+    bool skewed = false, constant = false;
+    if (!digits.empty()) LSB_TRY(first_hist(digits[0], &skewed, &constant));
+    LSB_TRY(onesweep_digits(c, r, digits, &passes));
+  }
+  return queue_err_word();
+}
+
+}  // namespace
+
+// Rank r alone (its local block); *passes gets the passes it ran, *varying the
+// key bits that vary in the block (0 for an empty block).
+int sort_local_rank(lsb_ctx* c, Rank& r, int* passes, uint64_t* varying) {
+  LocalSort s(c, r);
+  LSB_TRY(s.begin());
+  LSB_TRY(s.queue());
+  LSB_TRY(s.finish());
+  *passes = s.passes;
+  *varying = s.varying;
+  return LSB_OK;
+}
+
+// Every rank's local block, step by step across the ranks: c->last_local_passes
+// gets the most passes a rank ran, c->last_varying the bits that vary anywhere.
+int sort_local_ranks(lsb_ctx* c) {
+  std::deque<LocalSort> jobs;
+  for (Rank& r : c->ranks) jobs.emplace_back(c, r);
+  for (LocalSort& j : jobs) LSB_TRY(j.begin());
+  for (LocalSort& j : jobs) LSB_TRY(j.queue());
+  for (LocalSort& j : jobs) LSB_TRY(j.finish());
+  c->last_local_passes = 0;
+  c->last_varying = 0;
+  for (const LocalSort& j : jobs) {
+    c->last_local_passes = std::max(c->last_local_passes, j.passes);
+    c->last_varying |= j.varying;
+  }
   return LSB_OK;
 }
 
 int sort_onesweep(lsb_ctx* c) {
-  return sort_onesweep_rank(c, c->ranks[0], &c->last_local_passes, &c->last_varying);
-}
-// Rank r's block sorted on the whole key: single-read passes, or count + scan
-// + scatter when they do not apply.  Digits constant over the block are skipped.
-int sort_local_rank(lsb_ctx* c, Rank& r, int* passes, uint64_t* varying) {
-  *passes = 0;
-  *varying = 0;
-  if (r.here == 0) return LSB_OK;
-  if (c->onesweep && r.here <= lsb::kOnesweepMaxElems) return sort_onesweep_rank(c, r, passes, varying);
-  HIP_TRY(hipSetDevice(r.dev));
-  HIP_TRY(hipMemsetAsync(r.span, 0, 2 * sizeof(uint64_t), r.stream));
-  c->pass_cursor = 0;
-  begin_pass(c, 0);
-  LSB_TRY(local_pass(c, r, 0, c->skip_constant));
-  *passes = 1;
-  *varying = ~0ull;
-  if (c->skip_constant) {
-    HIP_TRY(hipMemcpyAsync(r.span_h, r.span, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, r.stream));
-    HIP_TRY(hipStreamSynchronize(r.stream));
-    *varying = r.span_h[0] & r.span_h[1];
-  }
-  for (int d = 1; d < 64 / lsb::kDigitBits; ++d) {
-    if (((*varying >> (d * lsb::kDigitBits)) & (lsb::kBuckets - 1)) == 0) continue;
-    begin_pass(c, d * lsb::kDigitBits);
-    LSB_TRY(local_pass(c, r, d * lsb::kDigitBits));
-    ++*passes;
-  }
-  return LSB_OK;
+  return sort_local_rank(c, c->ranks[0], &c->last_local_passes, &c->last_varying);
 }
 
 // After a stream sync: did a look-back give up?  (Never expected: every

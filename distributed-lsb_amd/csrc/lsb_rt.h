@@ -314,10 +314,9 @@ int onesweep_launch(lsb_ctx* c, Rank& r, int shift, int next, const uint32_t* hi
                     uint32_t* next_hist, lsb::OnesweepExtra x);
 int queue_halves(lsb_ctx* c, Rank& r, const uint32_t* hist);
 int choose_halves(lsb_ctx* c, Rank& r, bool synced);
-int sort_onesweep_rank(lsb_ctx* c, Rank& r, int* passes, uint64_t* varying);
-int sort_hybrid_rank(lsb_ctx* c, Rank& r, int* passes, uint64_t* varying);
 int sort_onesweep(lsb_ctx* c);
 int sort_local_rank(lsb_ctx* c, Rank& r, int* passes, uint64_t* varying);
+int sort_local_ranks(lsb_ctx* c);  // every rank, step by step across ranks
 int onesweep_check(Rank& r);
 #ifdef LSB_OS_PROFILE
 void os_profile_report();

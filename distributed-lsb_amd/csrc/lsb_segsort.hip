@@ -1,5 +1,5 @@
 // Segmented local sort: the last pass of the hybrid local sort
-// (LSB_OPT_HYBRID; lsb_runtime.cpp sort_hybrid_rank).
+// (LSB_OPT_HYBRID; lsb_passes.cpp LocalSort).
 //
 // The reference sorts a rank's block by 64 / RADIX stable passes of
 // localShuffle (mpi/mpi_lsbsort.cpp:213-247, 580-585), least significant

@@ -319,15 +319,7 @@ int exchange_merge(lsb_ctx* c) {
 
 // lsb_sort / lsb_pass(0) with a 64-bit exchange digit on an exchanging context.
 int merge_sort(lsb_ctx* c) {
-  c->last_local_passes = 0;
-  c->last_varying = 0;
-  for (Rank& r : c->ranks) {
-    int passes = 0;
-    uint64_t varying = 0;
-    LSB_TRY(sort_local_rank(c, r, &passes, &varying));
-    c->last_local_passes = std::max(c->last_local_passes, passes);
-    c->last_varying |= varying;
-  }
+  LSB_TRY(sort_local_ranks(c));
   c->last_exchanges = 1;
   return exchange_merge(c);
 }

@@ -1,6 +1,6 @@
 """The N > 1 path with real processes on CPU (world size 2, gloo).
 
-Each rank runs the runtime's per-pass protocol (lsb_runtime.cpp
+Each rank runs the runtime's per-pass protocol (lsb_exchange.cpp
 exchange_rccl) with gloo standing in for RCCL and the oracle's local pass
 standing in for the device kernels:
   local stable pass -> all-gather of bucket counts -> lsb_plan_exchange
