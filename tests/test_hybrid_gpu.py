@@ -253,3 +253,26 @@ def test_failed_launch_mid_hybrid_keeps_the_context(lsb_built, oracle_mod, mode,
             w.generate()
             w.my_sort()
             assert w.verify() == (True, -1)
+
+
+@pytest.mark.parametrize("fail_at", [2, 4])
+def test_failed_launch_in_phased_local_sorts(lsb_built, oracle_mod, fail_at):
+    """The whole-key exchange's local sorts run step by step across a loopback
+    context's ranks (sort_local_ranks).  A launch that fails in rank 0's
+    passes (2) or rank 1's (4: each rank's 150,004 records take k = 3 byte
+    passes, queued rank after rank) leaves every rank's input in A, and the
+    next sort on the context is exact."""
+    n = 300_007
+    with lsb_built.World(n, ranks=2, radix_bits=64) as w:
+        w.set_option(lsb_built.OPT_HYBRID, 1)
+        w.generate()
+        inp = w.gather_global()
+        w.set_option(lsb_built.OPT_FAIL_ONESWEEP, fail_at)
+        with pytest.raises(lsb_built.LsbError, match="injected"):
+            w.my_sort()
+        assert np.array_equal(w.gather_global(), inp)
+        w.my_sort()
+        assert np.array_equal(w.gather_global(), oracle_mod.stable_sort(inp))
+        w.generate()
+        w.my_sort()
+        assert w.verify() == (True, -1)
