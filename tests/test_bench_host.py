@@ -131,3 +131,23 @@ def test_torchrun_ranks_run_the_extra_in_child_processes(fail_extra):
     else:
         assert out["whole_key_melem_s"] == 128.0
     assert out["peer_melem_s"] == 32.0 and out["exchange_roofline"]["exchanges_per_sort"] == 4
+
+
+def test_eight_rank_dry_launch():
+    """The driver's largest scaling case (N = 8, `python bench.py --gpus 8`)
+    through the whole host path: eight rank processes, the all-gathered
+    exchange stats of eight ranks (7 peers each), both extras in fresh
+    processes, one line from rank 0."""
+    r = _bench(["--gpus", "8", "--dry-rank", "--no-cpu-baseline", "--steps", "2", "--warmup", "1"],
+               timeout=420)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = _line(r.stdout)
+    assert out["n_gpus"] == 8 and out["max_rank"] == 7.0 and out["value"] == 8 * 16
+    assert out["whole_key_melem_s"] == 8 * 64 and out["whole_key_verified"] is True
+    assert out["peer_melem_s"] == 8 * 16 and out["peer_verified"] is True
+    x = out["exchange_roofline"]
+    mib = 1 << 20
+    # dry_stats: rank r sends (r + 1) MiB to each of its 7 peers per exchange
+    assert x["link_bytes_per_exchange"] == {"max": 8 * mib, "min": mib}
+    assert x["rank_bytes_per_sort"] == {"max": 7 * 4 * 8 * mib, "min": 7 * 4 * mib}
+    assert x["link_bytes_per_sort"]["max_link"][0] == 7 and x["link_bytes_per_sort"]["max_over_min"] == 8.0
