@@ -117,6 +117,15 @@ for s in $RUN; do
         done
       done
       python3 tools/pick_summary.py $O/kcand_c4.log $O/kcand_c8.log ;;
+    refine)  # a placement variant: the FIRST context of fresh processes, abtest/old vs the tree's build
+      for k in 1 2 3 4 5; do
+        for lib in old new; do
+          L=abtest/old/liblsb.so; [ $lib = new ] && L=distributed-lsb_amd/build/liblsb.so
+          LSB_LIBRARY=$L timeout -k 10 200 python -u tools/alloc_probe.py 30 1 3 \
+            >> $O/refine_$lib.log 2>&1 || fail refine $O/refine_$lib.log
+        done
+      done
+      python3 tools/pick_summary.py $O/refine_old.log $O/refine_new.log ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
