@@ -121,7 +121,9 @@ for s in $RUN; do
       for k in 1 2 3 4 5; do
         for lib in old new; do
           L=abtest/old/liblsb.so; [ $lib = new ] && L=distributed-lsb_amd/build/liblsb.so
-          LSB_LIBRARY=$L timeout -k 10 200 python -u tools/alloc_probe.py 30 1 3 \
+          [ -n "${REFINE_NEW_ENV:-}" ] && L=distributed-lsb_amd/build/liblsb.so
+          E=""; [ $lib = new ] && E="${REFINE_NEW_ENV:-}"
+          env $E LSB_LIBRARY=$L timeout -k 10 200 python -u tools/alloc_probe.py 30 1 3 \
             >> $O/refine_$lib.log 2>&1 || fail refine $O/refine_$lib.log
         done
       done
