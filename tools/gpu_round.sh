@@ -15,6 +15,7 @@
 #   sq        tools/sq_counters.sh: SQ counters of the sort at 2^28
 #   stress    tools/stress_mix.py for STRESS_S seconds (default 150): random sorts, 0 wrong
 #   dropin    tests/test_dropin_gpu.py alone (the reference program with its mySort on the library)
+#   (experiments: allocbw placement allocpmc abx pick rot clock kcand refine; see each case)
 # Output under gpurun_out/$TAG/.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
