@@ -120,7 +120,7 @@ int place_range(lsb_ctx* c, Rank& r, int shift, int src_rank, const Elem* src, i
   Timer t(c, &r, LSB_K_PLACE, r.pstream);
   HIP_TRY(lsb::launch_place(src, r.B, r.here, k0, cnt, shift, c->nb,
                             r.place + (size_t)src_rank * c->nb, r.pstream, r.place_next,
-                            r.place_hist, !r.gather_next));
+                            r.place_hist, !r.gather_next, r.os_halves == 2));
   return LSB_OK;
 }
 

@@ -218,10 +218,12 @@ hipError_t launch_segfix(const Elem* in, Elem* out, int64_t m, int shift, const 
 // next_hist[x * 256 + b] (x = the out position's onesweep sub-array over
 // out_len records; zeroed by the caller): the next local pass's sub_hist.
 // store = false (with next_shift >= 0): count only, out untouched (the next
-// pass gathers, GatherSrc).
+// pass gathers, GatherSrc).  skew: the sort's keys are skewed (its stage
+// split): the count adds once per run of equal counters.
 hipError_t launch_place(const Elem* src, Elem* out, int64_t out_len, int64_t k0, int64_t count,
                         int shift, int nbuckets, const int64_t* off_row, hipStream_t s,
-                        int next_shift = -1, uint32_t* next_hist = nullptr, bool store = true);
+                        int next_shift = -1, uint32_t* next_hist = nullptr, bool store = true,
+                        bool skew = false);
 
 // Peer-store exchange (opt-in, LSB_OPT_EXCHANGE_PEER): from the all-gathered
 // counts hist[s * nb + b], rank `me` writes each of its m bucket-ordered

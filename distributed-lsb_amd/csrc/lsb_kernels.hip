@@ -1264,6 +1264,25 @@ __device__ __forceinline__ void onesweep_body(
         }
         const uint32_t d = (uint32_t)(v.key >> shift) & (kBuckets - 1);
         emit(skew_tag, v, j, delta[d] + pos, NEXT ? cut[d] : 0u);
+        if (C16 && mixed16) {
+          // The tile crosses a low-byte boundary: its 16-bit digit counts by
+          // runs of equal (digit, low byte) slots within each wave-instruction
+          // (the stage is in that order), one add per run by its head lane,
+          // instead of thread t walking its whole bucket run alone (a hot
+          // key's run kept its workgroup, and the tile it had already
+          // reserved, for the length of the walk).  Active lanes are a
+          // prefix, as in emit's skewed count.
+          const uint32_t s16 = (d << 8) | ((uint32_t)(v.key >> shift16) & 0xFFu);
+          const uint64_t act = __ballot(1);
+          const uint32_t prev = (uint32_t)__builtin_amdgcn_update_dpp((int)~s16, (int)s16, 0x138, 0xf, 0xf, false);
+          const bool head = prev != s16;
+          const uint64_t heads = __ballot(head);
+          if (head) {
+            const uint64_t above = heads & ~((2ull << lane) - 1ull);
+            const uint32_t end = above ? (uint32_t)__builtin_ctzll(above) : (uint32_t)__popcll(act);
+            atomicAdd(count16 + s16, (unsigned long long)(end - lane));
+          }
+        }
       }
     };
     for (int h = 0; h < HALVES; ++h) {
@@ -1273,18 +1292,6 @@ __device__ __forceinline__ void onesweep_body(
       }
       if (skewed) write_out(std::true_type{}, h);
       else write_out(std::false_type{}, h);
-      if (C16 && mixed16) {  // the tile crosses a low-byte boundary: walk run t
-        const uint32_t k0 = lstart > (uint32_t)(h * HT) ? lstart : (uint32_t)(h * HT);
-        const uint32_t k1 = lstart + cnt < (uint32_t)((h + 1) * HT) ? lstart + cnt : (uint32_t)((h + 1) * HT);
-        for (uint32_t k = k0; k < k1; ++k) {
-          const uint32_t l = (uint32_t)(stage[k - h * HT].key >> shift16) & 0xFFu;
-          if (l != acc_lo) {
-            c16_flush();
-            acc_lo = l;
-          }
-          ++acc;
-        }
-      }
       // After wave 0's writes: the grab has returned by then.
       if (h == HALVES - 1) fetch_desc();
       __syncthreads();
@@ -1355,7 +1362,7 @@ __global__ __launch_bounds__(kPlaceBlock) void k_place(const Elem* __restrict__ 
                                                        int64_t count, int shift, uint32_t mask,
                                                        const int64_t* __restrict__ off_row,
                                                        int64_t out_len, int next_shift,
-                                                       uint32_t* __restrict__ next_hist) {
+                                                       uint32_t* __restrict__ next_hist, uint32_t skew) {
   __shared__ int64_t lds_off[kLds ? kPlaceLdsBuckets : 1];
   __shared__ uint32_t nh[kNext ? kSub * kBuckets : 1];
   const int nb = (int)mask + 1;
@@ -1389,7 +1396,28 @@ __global__ __launch_bounds__(kPlaceBlock) void k_place(const Elem* __restrict__ 
         if (kStore) store_elem(out + g, x[i]);
         if (kNext) {
           const uint32_t xs = (uint32_t)sub_of_tile(g / kTile, TT);
-          atomicAdd(&nh[xs * kBuckets + ((uint32_t)(x[i].key >> next_shift) & (kBuckets - 1))], 1u);
+          const uint32_t slot = xs * kBuckets + ((uint32_t)(x[i].key >> next_shift) & (kBuckets - 1));
+          if (skew) {
+            // Skewed keys (the sort's stage split): one add per run of equal
+            // slots within the wave-instruction, as k_onesweep's skewed count
+            // (a source's records arrive in digit order, so hot keys come in
+            // runs; active lanes are a prefix).  64 lanes adding to one LDS
+            // counter cost 50 conflict cycles per instruction (Zipf, forced
+            // 16-bit exchange: the count 3.43 vs 3.07 ms uniform).
+            const uint64_t act = __ballot(1);
+            const uint32_t lane = lane_id();
+            const uint32_t prev =
+                (uint32_t)__builtin_amdgcn_update_dpp((int)~slot, (int)slot, 0x138, 0xf, 0xf, false);
+            const bool head = prev != slot;
+            const uint64_t heads = __ballot(head);
+            if (head) {
+              const uint64_t above = heads & ~((2ull << lane) - 1ull);
+              const uint32_t end = above ? (uint32_t)__builtin_ctzll(above) : (uint32_t)__popcll(act);
+              atomicAdd(&nh[slot], end - lane);
+            }
+          } else {
+            atomicAdd(&nh[slot], 1u);
+          }
         }
       }
     }
@@ -1982,7 +2010,7 @@ hipError_t launch_onesweep(const Elem* in, Elem* out, int64_t m, int shift, int 
 
 hipError_t launch_place(const Elem* src, Elem* out, int64_t out_len, int64_t k0, int64_t count,
                         int shift, int nbuckets, const int64_t* off_row, hipStream_t s,
-                        int next_shift, uint32_t* next_hist, bool store) {
+                        int next_shift, uint32_t* next_hist, bool store, bool skew) {
   if (count <= 0) return hipSuccess;
   if (nbuckets != 256 && nbuckets != 65536) return hipErrorInvalidValue;
   if (k0 < 0 || k0 + count > out_len) return hipErrorInvalidValue;
@@ -1995,28 +2023,28 @@ hipError_t launch_place(const Elem* src, Elem* out, int64_t out_len, int64_t k0,
     if (!store) {
       if (lds)
         hipLaunchKernelGGL((k_place<true, true, false>), grid, dim3(kPlaceBlock), 0, s, src, out, k0,
-                           count, shift, mask, off_row, out_len, next_shift, next_hist);
+                           count, shift, mask, off_row, out_len, next_shift, next_hist, skew ? 1u : 0u);
       else
         hipLaunchKernelGGL((k_place<false, true, false>), grid, dim3(kPlaceBlock), 0, s, src, out, k0,
-                           count, shift, mask, off_row, out_len, next_shift, next_hist);
+                           count, shift, mask, off_row, out_len, next_shift, next_hist, skew ? 1u : 0u);
       return hipGetLastError();
     }
     if (lds)
       hipLaunchKernelGGL((k_place<true, true>), grid, dim3(kPlaceBlock), 0, s, src, out, k0, count,
-                         shift, mask, off_row, out_len, next_shift, next_hist);
+                         shift, mask, off_row, out_len, next_shift, next_hist, skew ? 1u : 0u);
     else
       hipLaunchKernelGGL((k_place<false, true>), grid, dim3(kPlaceBlock), 0, s, src, out, k0, count,
-                         shift, mask, off_row, out_len, next_shift, next_hist);
+                         shift, mask, off_row, out_len, next_shift, next_hist, skew ? 1u : 0u);
     return hipGetLastError();
   }
   if (!store) return hipErrorInvalidValue;  // nothing to count
   const dim3 grid(grid_for(count, kPlaceBlock * kPlaceIpt, 4096));
   if (lds)
     hipLaunchKernelGGL((k_place<true, false>), grid, dim3(kPlaceBlock), 0, s, src, out, k0, count,
-                       shift, mask, off_row, out_len, 0, nullptr);
+                       shift, mask, off_row, out_len, 0, nullptr, 0u);
   else
     hipLaunchKernelGGL((k_place<false, false>), grid, dim3(kPlaceBlock), 0, s, src, out, k0, count,
-                       shift, mask, off_row, out_len, 0, nullptr);
+                       shift, mask, off_row, out_len, 0, nullptr, 0u);
   return hipGetLastError();
 }
 
