@@ -952,12 +952,30 @@ __device__ __forceinline__ void onesweep_body(
                                         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a));
           pb[k] = ((sel >> k) & 1u ? gs.A : gs.R) + (tb + adj);
         }
+        // A wave's load i covers tile positions [g0, g0 + 64): when one piece
+        // holds them all (every load but the <= 3 that straddle a piece
+        // start), its base is picked by scalar compares, not per lane
+        // (forced 16-bit exchange: -0.3 % uniform, -0.7 % Zipf per sort,
+        // profiles/r04/ab_gu/).
+        const int wu = __builtin_amdgcn_readfirstlane(w);
 #pragma unroll
         for (int i = 0; i < IPT; ++i) {
           const int li = wbase + i * 64;
-          const Elem* src = pb[0];
+          const int g0 = wu * 64 * IPT + i * 64;
+          int ka = 0, kb = 0;
 #pragma unroll
-          for (int k = 1; k < kDescPieces; ++k) src = li >= st[k] ? pb[k] : src;
+          for (int k = 1; k < kDescPieces; ++k) {
+            ka += g0 >= st[k] ? 1 : 0;
+            kb += g0 + 63 >= st[k] ? 1 : 0;
+          }
+          const Elem* src = pb[0];
+          if (ka == kb) {
+#pragma unroll
+            for (int k = 1; k < kDescPieces; ++k) src = ka >= k ? pb[k] : src;
+          } else {
+#pragma unroll
+            for (int k = 1; k < kDescPieces; ++k) src = li >= st[k] ? pb[k] : src;
+          }
           e[i] = li < nvalid ? load_elem_nt(src + li) : Elem{0ull, 0ull};
         }
       } else {
