@@ -84,6 +84,8 @@ def parse():
     ap.add_argument("--dry-fail", type=int, default=-1, help=argparse.SUPPRESS)
     ap.add_argument("--dry-fail-whole-key", type=int, default=-1, help=argparse.SUPPRESS)
     ap.add_argument("--dry-fail-peer", type=int, default=-1, help=argparse.SUPPRESS)
+    ap.add_argument("--dry-fail-x16", type=int, default=-1, help=argparse.SUPPRESS)
+    ap.add_argument("--dry-unverified", default="", help=argparse.SUPPRESS)
     ap.add_argument("--rank-timeout", type=int, default=1500,
                     help="self-launched rank processes: seconds before they are stopped")
     ap.add_argument("--no-verify", action="store_true")
@@ -106,7 +108,12 @@ def parse():
                          "hybrid (single-read passes on the top bytes, then one segmented local sort; "
                          "LSB_OPT_HYBRID, P = 1 and the whole-key form's local sorts)")
     ap.add_argument("--no-extras", action="store_true",
-                    help="skip the extra forms timed after the headline (hybrid at N = 1, whole key at N > 1)")
+                    help="skip the extra forms timed after the headline (hybrid and x16 at N = 1, whole key "
+                         "and peer at N > 1)")
+    ap.add_argument("--force-exchange", action="store_true",
+                    help="N = 1: run the exchange path anyway, over a world-of-one RCCL communicator that "
+                         "carries every record through ncclAllToAllv (LSB_OPT_FORCE_EXCHANGE + "
+                         "LSB_OPT_EXCHANGE_SELF); the x16 extra is this with --radix-bits 16")
     return ap.parse_args()
 
 
@@ -409,6 +416,15 @@ def make_world(a, d, N, n_total, radix):
         uid = lsbsort.get_unique_id() if d.rank == 0 else None
         uid = d.bcast_bytes(uid)
         w = lsbsort.World.rank(n_total, N, d.rank, device, uid, radix_bits=radix)
+    elif a.force_exchange:
+        # One rank of a world of one: the exchange path with the rank's own
+        # records through RCCL (BASELINE configs[4]'s exchange structure).
+        if N != 1:
+            raise SystemExit("--force-exchange is a one-GPU form")
+        device = 0
+        w = lsbsort.World.rank(n_total, 1, 0, device, lsbsort.get_unique_id(), radix_bits=radix)
+        w.set_option(lsbsort.OPT_FORCE_EXCHANGE, 1)
+        w.set_option(lsbsort.OPT_EXCHANGE_SELF, 1)
     else:
         if N != 1:
             raise SystemExit("multi-GPU runs are launched one process per GPU (torch.distributed.run)")
@@ -568,7 +584,12 @@ def extras_at(a, N):
         return []
     radix = a.radix_bits or (8 if N == 1 else 16)
     if N == 1:
-        return [("hybrid", extra_argv(a, ["--passes", "hybrid"]))] if a.passes == "onesweep" else []
+        if a.passes != "onesweep" or a.force_exchange:
+            return []
+        # the hybrid local sort, and the forced 16-bit exchange (x16): the
+        # reference's own digit (configs[4]) with its exchange path run
+        return [("hybrid", extra_argv(a, ["--passes", "hybrid"])),
+                ("x16", extra_argv(a, ["--force-exchange", "--radix-bits", "16"]))]
     out = []
     if radix != 64 and not a.no_whole_key:
         out.append(("whole_key", whole_key_argv(a)))
@@ -577,14 +598,45 @@ def extras_at(a, N):
     return out
 
 
+def any_unverified(out):
+    """The headline or any extra form produced output that failed lsb_verify
+    (an extra that failed to run is `<name>_error`, not a wrong answer)."""
+    return out.get("verified") is False or any(
+        k.endswith("_verified") and v is False for k, v in out.items())
+
+
+C5_BYTES_PER_ELEM = 192  # SURVEY.md 8(d): configs[4], 48 B per record per pass, 4 passes
+
+
+def c5_keys(out, n):
+    """N = 1: BASELINE configs[4] (the reference's 16-bit digits, 4 passes)
+    against SURVEY 8(d)'s C5 denominator (192 B per record).  At P = 1 a
+    16-bit digit runs as two stable 8-bit passes, so `--radix-bits 16`
+    alone is the headline's work; the forms that are C5's own answer are the
+    hybrid (4 byte passes over HBM plus one segmented sort) and the x16 extra
+    (the 16-bit exchange path run through RCCL)."""
+    for name in ("hybrid", "x16"):
+        ms = out.get(f"{name}_ms_per_step")
+        if ms:
+            out[f"{name}_c5_survey_frac"] = round(C5_BYTES_PER_ELEM * n / (ms / 1e3) / (HBM_PEAK_GBS * 1e9), 4)
+    out["c5_basis"] = ("SURVEY.md 8(d) C5: 192 B per record (48 B x 4 passes of 16-bit digits) / sort time / "
+                       "8 TB/s; at P = 1 a 16-bit digit runs as two stable 8-bit passes (a 65536-bucket "
+                       "pass is write-bound, DESIGN.md 5.15), so C5's answers are hybrid_* (4 byte passes + "
+                       "one segmented sort, same output) and x16_* (the 16-bit exchange path through RCCL)")
+
+
 def merge_extra(out, name, ok, text, report):
     """An extra form's keys into the headline line: <name>_melem_s,
     _ms_per_step, _verified (and its per-pass rows and dominant-kernel
     roofline when it has them), or <name>_error."""
-    r = last_json(text) if ok else None
+    r = last_json(text)
+    if r is not None and not ok and r.get("verified") is not False:
+        r = None  # a failed form's line counts only to say its output was wrong
     if r is None:
         out[f"{name}_error"] = report or "no result line"
         return
+    if not ok:
+        out[f"{name}_error"] = report or "failed"
     out[f"{name}_melem_s"] = r["value"]
     out[f"{name}_ms_per_step"] = r["ms_per_step"]
     out[f"{name}_verified"] = r["verified"]
@@ -610,10 +662,10 @@ def rank_extra(a, d, out, name, argv):
 def dry_stats(rank, P, steps):
     """Exchange stats of the shape lsb_get_exchange_stats reports, made up
     for --dry-rank (rank r sends (r + 1) MB to every peer per exchange)."""
-    per = [0 if q == rank else (rank + 1) << 20 for q in range(P)]
+    per = [0 if q == rank and P > 1 else (rank + 1) << 20 for q in range(P)]  # P = 1: to itself
     ex = 4 * steps
     return {"exchanges": ex, "calls": 4 * ex, "sent_bytes": [b * ex for b in per],
-            "recv_bytes": [0 if q == rank else ((q + 1) << 20) * ex for q in range(P)],
+            "recv_bytes": [0 if q == rank and P > 1 else ((q + 1) << 20) * ex for q in range(P)],
             "wire_ms": 1.0 * ex, "plan_ms": 0.1 * ex, "place_ms": 0.5 * ex, "place_tail_ms": 0.125 * ex,
             "place_bytes": 32 * 1000 * ex, "placed_records": 1000 * steps, "counted_records": 3000 * steps}
 
@@ -626,22 +678,35 @@ def dry_run(a):
     --dry-fail-whole-key / --dry-fail-peer R rank R of that extra)."""
     d = Dist()
     radix = a.radix_bits or (8 if d.world == 1 else 16)
-    fail = a.dry_fail_whole_key if radix == 64 else a.dry_fail_peer if a.exchange == "peer" else a.dry_fail
+    fail = (a.dry_fail_whole_key if radix == 64 else a.dry_fail_peer if a.exchange == "peer" else
+            a.dry_fail_x16 if a.force_exchange else a.dry_fail)
     if d.rank == fail:
         sys.exit(3)
     top = d.max(float(d.rank))
-    out = {"metric": METRIC, "value": float(d.world * radix), "ms_per_step": 1.0, "verified": True,
+    form = ("x16" if a.force_exchange else "whole_key" if radix == 64 and d.world > 1 else
+            "peer" if a.exchange == "peer" else "hybrid" if a.passes == "hybrid" else "headline")
+    out = {"metric": METRIC, "value": float(d.world * radix), "ms_per_step": 1.0,
+           "verified": form != a.dry_unverified,
            "n_gpus": d.world, "max_rank": top, "radix_bits": radix, "exchange": a.exchange,
            "config": {"n_total": a.n_per_gpu * d.world}}
-    if d.world > 1:
+    if d.world > 1 or a.force_exchange:
         out["exchange_roofline"] = exchange_roofline(
             d.all_gather_obj({"stats": dry_stats(d.rank, d.world, a.steps)}), a.steps)
+        out["per_pass"] = [{"pass": 0, "shift": 0, "kernel": "k_onesweep", "ms": 1.0, "exchange_ms": 0.5,
+                            "place_ms": 0.25, "wire_ms": 0.5, "place_tail_ms": 0.125}]
+    if d.world > 1:
         for name, argv in extras_at(a, d.world):
             rank_extra(a, d, out, name, argv)
+    else:
+        for name, argv in extras_at(a, 1):
+            merge_extra(out, name, *spawn_ranks(argv, [dict(os.environ)], extra_timeout(a), f"{name} extra"))
+        c5_keys(out, a.n_per_gpu)
     d.barrier()
     d.close()
     if d.rank == 0:
         print(json.dumps(out), flush=True)
+    if any_unverified(out):
+        sys.exit(1)
 
 
 def launch(a):
@@ -665,7 +730,7 @@ def launch(a):
                                             extra_timeout(a), f"{name} extra"))
     out["cpu_baseline"] = None if a.no_cpu_baseline else cpu_baseline(out["config"]["n_total"], a.cpu_n)
     print(json.dumps(out), flush=True)
-    if out.get("verified") is False or out.get("whole_key_verified") is False:
+    if any_unverified(out):
         sys.exit(1)
 
 
@@ -695,7 +760,8 @@ def exchange_roofline(ranks, steps):
     P = len(ranks)
     st = [r["stats"] for r in ranks]
     S = [[st[s]["sent_bytes"][q] / steps for q in range(P)] for s in range(P)]
-    links = sorted((S[s][q], s, q) for s in range(P) for q in range(P) if q != s)
+    # P = 1 (--force-exchange): the one "link" is the rank to itself through RCCL
+    links = sorted((S[s][q], s, q) for s in range(P) for q in range(P) if q != s or P == 1)
     wire = [x["wire_ms"] / steps for x in st]
     ex = st[0]["exchanges"] / steps
 
@@ -704,15 +770,20 @@ def exchange_roofline(ranks, steps):
 
     hi, lo = links[-1], links[0]
     link_gbs = gbs(hi[0], wire[hi[1]])
-    sent = [sum(S[s][q] for q in range(P) if q != s) for s in range(P)]
+    sent = [sum(S[s][q] for q in range(P) if q != s or P == 1) for s in range(P)]
     gpu = [g for g in (gbs(sent[s], wire[s]) for s in range(P)) if g is not None]
     place_ms = [x["place_ms"] / steps for x in st]
     tail = [x["place_tail_ms"] / steps for x in st]
     pbytes = [x["place_bytes"] / steps for x in st]
     busy = max(range(P), key=lambda r: place_ms[r])
+    self_only = P == 1
     return {
-        "bound": "xgmi", "unit": "GB/s", "peak": XGMI_LINK_GBS, "peak_source": XGMI_PEAK_SOURCE,
-        "achieved": link_gbs, "frac": round(link_gbs / XGMI_LINK_GBS, 4) if link_gbs else None,
+        "bound": "self" if self_only else "xgmi", "unit": "GB/s",
+        "peak": None if self_only else XGMI_LINK_GBS,
+        "peak_source": ("one GPU: the rank's records go through RCCL to itself (a device copy, no link); "
+                        "no xGMI figure applies") if self_only else XGMI_PEAK_SOURCE,
+        "achieved": link_gbs,
+        "frac": round(link_gbs / XGMI_LINK_GBS, 4) if link_gbs and not self_only else None,
         "exchanges_per_sort": ex, "calls_per_sort": st[0]["calls"] / steps,
         "rank_bytes_per_sort": {"max": int(max(sent)), "min": int(min(sent))},
         "link_bytes_per_sort": {"max": int(hi[0]), "max_link": [hi[1], hi[2]],
@@ -794,7 +865,7 @@ def main():
     placement = w.placement()
     last = w.last_sort()
     w.close()
-    xroof = exchange_roofline(d.all_gather_obj({"stats": xstats}), a.steps) if N > 1 else None
+    xroof = exchange_roofline(d.all_gather_obj({"stats": xstats}), a.steps) if N > 1 or a.force_exchange else None
 
     ms_per_step = total / a.steps * 1e3
     value = n_total * a.steps / total / 1e6
@@ -805,7 +876,10 @@ def main():
         cfg = "configs[1]" if radix == 8 else "configs[4]"
         workload = (f"{cfg}: sort of {size} 16-byte records per GPU, {radix}-bit digits, "
                     f"{64 // radix} passes, {N} GPU(s)")
-        if radix == 16:
+        if radix == 16 and a.force_exchange:
+            workload += (" (each digit as two stable 8-bit sub-passes, then the digit's exchange: counts "
+                         "all-gather, plan, RCCL AllToAllv of every record to this rank itself, placement)")
+        elif radix == 16:
             workload += " (each digit as two stable 8-bit sub-passes; no exchange)"
     else:
         cfg = "configs[2]" if a.dist == "uniform" else "configs[3]"
@@ -890,7 +964,7 @@ def main():
                         "or counts all-gather + plan + all-to-all (per digit); includes wire time",
             "place": "placement stream: merge of the received runs (whole key) or k_place",
             "sort": "the whole sort, per rank"},
-        "exchange_bytes_per_step": xbytes // a.steps if N > 1 else 0,
+        "exchange_bytes_per_step": xbytes // a.steps if N > 1 or a.force_exchange else 0,
         "exchange_roofline": xroof,
         "placement": dict(placement, basis="rank 0's A and B, chosen at context creation among `candidates` "
                                             "buffers by one timed k_onesweep pass between every ordered pair; ms "
@@ -907,6 +981,8 @@ def main():
             rank_extra(a, d, out, name, xargv)
         else:
             merge_extra(out, name, *spawn_ranks(xargv, [dict(os.environ)], extra_timeout(a), f"{name} extra"))
+    if N == 1:
+        c5_keys(out, n_total)
     if d.rank == 0 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(n_total, a.cpu_n)
     elif d.rank == 0:
@@ -915,7 +991,7 @@ def main():
     d.close()
     if d.rank == 0:
         print(json.dumps(out), flush=True)
-    if verified is False or out.get("whole_key_verified") is False:
+    if any_unverified(out):
         sys.exit(1)
 
 

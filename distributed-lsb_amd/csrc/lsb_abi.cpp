@@ -44,6 +44,9 @@ int lsb_create(lsb_ctx_t** out, int64_t n_total, int num_ranks, const int* dev_i
   c->mode = Mode::kLoopback;
   c->first_rank = 0;
   c->ranks.resize(num_ranks);
+  for (int r = 0; r < num_ranks; ++r)
+    for (int q = 0; q < r; ++q)
+      if ((dev_ids ? dev_ids[r] : 0) == (dev_ids ? dev_ids[q] : 0)) c->shared_device = true;
   for (int r = 0; r < num_ranks; ++r) {
     int rc = init_rank(c, c->ranks[r], r, dev_ids ? dev_ids[r] : 0);
     if (rc != LSB_OK) {
@@ -144,7 +147,7 @@ void lsb_destroy(lsb_ctx_t* c) {
   os_profile_report();
 #endif
   for (Rank& r : c->ranks) free_rank(r);
-  for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
+  for (auto& e : c->event_pool) (void)hipEventDestroy(e.second);
   if (c->comm) (void)ncclCommDestroy(c->comm);
   delete c;
 }

@@ -5,6 +5,8 @@
 // caller's host callbacks) that the pass driver and both exchange forms use.
 #include "lsb_rt.h"
 
+#include <mutex>
+
 namespace lsb_rt {
 
 thread_local std::string g_last_error;
@@ -19,12 +21,17 @@ int fail(int code, const char* what, const char* detail) {
   return code;
 }
 // ---- timing -------------------------------------------------------------
+// An event of the current device: from the pool (events are filed under the
+// device they were created on), else a new one.
 hipEvent_t take_event(lsb_ctx* c) {
-  if (!c->event_pool.empty()) {
-    hipEvent_t e = c->event_pool.back();
-    c->event_pool.pop_back();
-    return e;
-  }
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  for (size_t i = c->event_pool.size(); i-- > 0;)
+    if (c->event_pool[i].first == dev) {
+      hipEvent_t e = c->event_pool[i].second;
+      c->event_pool.erase(c->event_pool.begin() + (long)i);
+      return e;
+    }
   hipEvent_t e = nullptr;
   if (hipEventCreate(&e) != hipSuccess) return nullptr;
   return e;
@@ -58,8 +65,8 @@ int resolve_timing(lsb_ctx* c) {
       c->pass_launches[p.pass][p.kid] += 1;
       c->pass_ms[p.pass][p.kid] += ms;
     }
-    c->event_pool.push_back(p.start);
-    c->event_pool.push_back(p.stop);
+    c->event_pool.push_back({p.dev, p.start});
+    c->event_pool.push_back({p.dev, p.stop});
   }
   c->pending.clear();
   return LSB_OK;
@@ -73,27 +80,162 @@ int max_chunks_for_device(int dev) {
   return std::min(lsb::kMaxChunks, 2 * prop.multiProcessorCount);
 }
 
-// ---- record buffers A and B, placement-calibrated ----------------------------
-// How fast an LSD pass streams between two 16 GiB record buffers depends on
-// where the driver placed them: per buffer the write side runs
-// at 5.6-6.9 TB/s (tools/kbench/allocbw.hip, profiles/r04/allocbw_*.log), and
-// k_onesweep's passes at 6.7-7.3 ms between pairs allocated in one process
-// (profiles/r04/v5_pick.log).  So a rank's A and B are chosen among K
-// candidate buffers by timing one k_onesweep pass between every ordered pair;
-// the pair with the smallest sum of both directions (the passes ping-pong) is
-// kept and the rest are freed.  K = LSB_PLACEMENT_CANDIDATES (environment,
-// default 8; 2 or less: A and B as allocated), for buffers of at least 1 GiB
-// and only as many as fit in 90 % of the free memory.  Eight candidates found
-// a pair at 6.71-6.72 ms in each of four fresh processes, where four found one
-// only in two of four (profiles/r04/v6_kcand_c{4,8}.log).  Cost at 2^30
-// records: ~0.7 s at context creation, 128 GiB held while it runs.
+// ---- record buffers: physical memory in 1 GiB pieces ---------------------------
+// A record buffer of at least one piece (LSB_VMM_CHUNK_MIB, default 1024) is
+// not a hipMalloc: its address range is reserved once and backed by
+// separately created 1 GiB physical allocations (hipMemCreate + hipMemMap,
+// HIP's virtual memory management).  The same LSD write pattern between two
+// hipMalloc'd 16 GiB buffers runs at 6.85 ms for most pairs and 7.2 ms for
+// some (the driver's choice of physical pages), while between buffers built
+// from 1 GiB pieces it runs at 5.7-6.8 ms (tools/kbench/vmmbw.hip,
+// profiles/r05/vmm_*; DESIGN.md §4 "Spread").  LSB_RECORD_ALLOC=malloc keeps
+// hipMalloc.  Pieces are readable and writable by every device that can
+// access this one (hipMemSetAccess), as hipMalloc memory is once peer access
+// is enabled; IPC handles cannot name them, so the peer-store exchange moves
+// the records into hipMalloc buffers at its setup (peer_setup).
 namespace {
 
-// How many candidate buffers of `bytes` to try (<= 2: no probing).
-int placement_candidates(double bytes, int want) {
-  int K = want;
+struct VmmBuffer {
+  void* base = nullptr;
+  size_t bytes = 0;
+  size_t piece = 0;
+  std::vector<hipMemGenericAllocationHandle_t> pieces;
+};
+std::mutex g_vmm_mu;
+std::vector<VmmBuffer> g_vmm;  // live VMM record buffers of this process
+
+size_t vmm_piece_bytes() {
+  const char* mode = getenv("LSB_RECORD_ALLOC");
+  if (mode && strcmp(mode, "malloc") == 0) return 0;
+  size_t mib = 1024;
+  if (const char* e = getenv("LSB_VMM_CHUNK_MIB")) mib = (size_t)std::max(0ll, atoll(e));
+  return mib << 20;
+}
+
+// Unmaps and releases the first pieces.size() pieces of `piece` bytes (mapped
+// in order from the base) and frees the address range.
+void vmm_release(VmmBuffer& b, size_t piece) {
+  for (size_t k = 0; k < b.pieces.size(); ++k) (void)hipMemUnmap(static_cast<char*>(b.base) + k * piece, piece);
+  for (auto h : b.pieces) (void)hipMemRelease(h);
+  if (b.base) (void)hipMemAddressFree(b.base, b.bytes);
+  (void)hipGetLastError();
+  b = VmmBuffer();
+}
+
+}  // namespace
+
+bool rec_is_vmm(const void* p) {
+  std::lock_guard<std::mutex> lock(g_vmm_mu);
+  for (const VmmBuffer& b : g_vmm)
+    if (b.base == p) return true;
+  return false;
+}
+
+int rec_alloc(Elem** out, size_t count) {
+  *out = nullptr;
+  const size_t piece = vmm_piece_bytes();
+  const size_t want = std::max<size_t>(count, 1) * sizeof(Elem);
+  if (piece == 0 || want < piece) return dev_alloc(out, count);
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  hipMemAllocationProp prop = {};
+  prop.type = hipMemAllocationTypePinned;
+  prop.location.type = hipMemLocationTypeDevice;
+  prop.location.id = dev;
+  size_t gran = 0;
+  HIP_TRY(hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum));
+  if (gran == 0 || piece % gran) return fail(LSB_ERR_INVALID, "rec_alloc", "LSB_VMM_CHUNK_MIB is not a multiple of the granularity");
+  VmmBuffer b;
+  b.bytes = (want + piece - 1) / piece * piece;
+  hipError_t e = hipMemAddressReserve(&b.base, b.bytes, piece, nullptr, 0);
+  if (e != hipSuccess) {
+    b.base = nullptr;
+    return fail(LSB_ERR_NOMEM, "hipMemAddressReserve", hipGetErrorString(e));
+  }
+  for (size_t off = 0; off < b.bytes; off += piece) {
+    hipMemGenericAllocationHandle_t h;
+    e = hipMemCreate(&h, piece, &prop, 0);
+    if (e != hipSuccess) break;
+    b.pieces.push_back(h);
+    e = hipMemMap(static_cast<char*>(b.base) + off, piece, 0, h, 0);
+    if (e != hipSuccess) {
+      (void)hipMemRelease(h);
+      b.pieces.pop_back();
+      break;
+    }
+  }
+  if (e == hipSuccess) {
+    // this device, and every device that can reach it (as peer access does for hipMalloc)
+    int ndev = 0;
+    (void)hipGetDeviceCount(&ndev);
+    std::vector<hipMemAccessDesc> acc;
+    for (int k = -1; k < ndev; ++k) {  // the owner first
+      const int d = k < 0 ? dev : k;
+      int can = k < 0;
+      if (k >= 0 && (d == dev || hipDeviceCanAccessPeer(&can, d, dev) != hipSuccess)) can = 0;
+      if (!can) continue;
+      hipMemAccessDesc a = {};
+      a.location.type = hipMemLocationTypeDevice;
+      a.location.id = d;
+      a.flags = hipMemAccessFlagsProtReadWrite;
+      acc.push_back(a);
+    }
+    e = hipMemSetAccess(b.base, b.bytes, acc.data(), acc.size());
+    if (e != hipSuccess && acc.size() > 1) e = hipMemSetAccess(b.base, b.bytes, acc.data(), 1);  // owner only
+  }
+  if (e != hipSuccess) {
+    const std::string why = hipGetErrorString(e);
+    vmm_release(b, piece);
+    return fail(LSB_ERR_NOMEM, "rec_alloc (hipMemCreate / hipMemMap / hipMemSetAccess)", why.c_str());
+  }
+  b.piece = piece;
+  *out = static_cast<Elem*>(b.base);
+  std::lock_guard<std::mutex> lock(g_vmm_mu);
+  g_vmm.push_back(std::move(b));
+  return LSB_OK;
+}
+
+void rec_free(void* p) {
+  if (!p) return;
+  VmmBuffer b;
+  {
+    std::lock_guard<std::mutex> lock(g_vmm_mu);
+    for (size_t i = 0; i < g_vmm.size(); ++i)
+      if (g_vmm[i].base == p) {
+        b = std::move(g_vmm[i]);
+        g_vmm.erase(g_vmm.begin() + (long)i);
+        break;
+      }
+  }
+  if (!b.base) {
+    (void)hipFree(p);
+    return;
+  }
+  vmm_release(b, b.piece);
+}
+
+// ---- record buffers A and B: the optional placement probe -----------------------
+// Before round 5 the record buffers were hipMalloc'd, and how fast an LSD pass
+// streamed between two of them depended on where the driver placed them: the
+// pass ran at 6.7-7.3 ms between pairs allocated in one process
+// (profiles/r04/v5_pick.log).  Round 4 therefore chose A and B among 8
+// candidate buffers by timing one k_onesweep pass between every ordered pair
+// (~0.7 s and 128 GiB at context creation at 2^30 records).  Buffers built
+// from 1 GiB VMM pieces (rec_alloc) run every pass at 6.69-6.71 ms on average
+// in each of five fresh processes with no probe, where hipMalloc'd pairs ran
+// at 6.71, 6.99 and 7.27 (profiles/r05/alloc_sweep.log), so the probe is now
+// opt-in: LSB_PLACEMENT_CANDIDATES = K > 2 (at most 8) still tries K
+// candidates for A and B (and min(K, 3) for R), for buffers of at least
+// 1 GiB, as many as fit in 90 % of the free memory, and never when another
+// rank of this context shares the device (its timings would be the other
+// rank's too, and the candidates its memory).
+namespace {
+
+// How many candidate buffers of `bytes` to try, at most `cap` (<= 2: no probing).
+int placement_candidates(double bytes, int cap) {
+  int K = 0;
   if (const char* e = getenv("LSB_PLACEMENT_CANDIDATES")) K = atoi(e);
-  K = std::min(K, 8);
+  K = std::min(K, cap);
   size_t free_b = 0, total_b = 0;
   if (K > 2 && bytes >= (double)(1ull << 30) && hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
     while (K > 2 && K * bytes > 0.9 * (double)free_b) --K;
@@ -125,12 +267,12 @@ int alloc_candidates(size_t per, int K, size_t need, std::vector<Elem*>& cand) {
   cand.clear();
   for (int k = 0; k < K; ++k) {
     Elem* p = nullptr;
-    if (dev_alloc(&p, per) != LSB_OK) break;  // fewer candidates than hoped
+    if (rec_alloc(&p, per) != LSB_OK) break;  // fewer candidates than hoped
     cand.push_back(p);
   }
   (void)hipGetLastError();
   if (cand.size() >= need) return LSB_OK;
-  for (Elem* p : cand) (void)hipFree(p);
+  for (Elem* p : cand) rec_free(p);
   cand.clear();
   return fail(LSB_ERR_NOMEM, "alloc_candidates", "record buffers");
 }
@@ -167,19 +309,33 @@ double time_pass(Rank& r, Prober& pr, const Elem* x, Elem* y, int shift, uint32_
 // (tools/kbench/allocbw.hip) ranked the buffers by their streaming write speed, but
 // that did not predict the pass, whose tile loads sit on its look-back chain
 // (profiles/r04/placement_*.log, pick.log).
+// After a probe: a probe pass that gave up on its look-back leaves the sort's
+// give-up word set and its status rows of an older parity.  Start them over
+// (as onesweep_check does) and fail the creation rather than hand the next
+// sort a false error.
+int probe_check(Rank& r) {
+  uint32_t w = 0;
+  HIP_TRY(hipMemcpy(&w, r.os_ctr + lsb::kOnesweepSubs, sizeof w, hipMemcpyDeviceToHost));
+  if (w == 0) return LSB_OK;
+  HIP_TRY(hipMemset(r.os_ctr + lsb::kOnesweepSubs, 0, sizeof(uint32_t)));
+  HIP_TRY(hipMemset(r.os_status, 0, (size_t)lsb::onesweep_tiles(r.here) * lsb::kBuckets * sizeof(uint32_t)));
+  r.os_epoch = 0;
+  return fail(LSB_ERR_HIP, "placement probe", "k_onesweep look-back timed out");
+}
+
 int alloc_records(lsb_ctx* c, Rank& r) {
   const size_t per = (size_t)c->per;
-  int K = placement_candidates((double)per * sizeof(Elem), 8);
+  int K = c->shared_device ? 0 : placement_candidates((double)per * sizeof(Elem), 8);
   r.placement_k = 0;
   if (K <= 2 || r.here < (int64_t)lsb::kTile * lsb::kOnesweepSubs || r.here > lsb::kOnesweepMaxElems) {
-    LSB_TRY(dev_alloc(&r.A, per));
-    return dev_alloc(&r.B, per);
+    LSB_TRY(rec_alloc(&r.A, per));
+    return rec_alloc(&r.B, per);
   }
   std::vector<Elem*> cand;
   LSB_TRY(alloc_candidates(per, K, 2, cand));
   K = (int)cand.size();
   auto give_up = [&](int rc) {
-    for (Elem* p : cand) (void)hipFree(p);
+    for (Elem* p : cand) rec_free(p);
     return rc;
   };
   int rc = onesweep_ensure(r);
@@ -199,6 +355,8 @@ int alloc_records(lsb_ctx* c, Rank& r) {
       sorted_by[y] = shift;
     }
   if (pr.err != hipSuccess) return give_up(fail(LSB_ERR_HIP, "alloc_records: placement probe", hipGetErrorString(pr.err)));
+  rc = probe_check(r);
+  if (rc != LSB_OK) return give_up(rc);
   // LSB_PLACEMENT_PICK=worst keeps the slowest pair instead (experiments:
   // tools/alloc_probe.py checks that the probe predicts the passes).
   const char* pick = getenv("LSB_PLACEMENT_PICK");
@@ -230,7 +388,7 @@ int alloc_records(lsb_ctx* c, Rank& r) {
   r.A = cand[bx];
   r.B = cand[by];
   for (Elem* p : cand)
-    if (p != r.A && p != r.B) (void)hipFree(p);
+    if (p != r.A && p != r.B) rec_free(p);
   return LSB_OK;
 }
 
@@ -242,9 +400,9 @@ int alloc_records(lsb_ctx* c, Rank& r) {
 // histogram of its own, since a sort may hold one in r.os_hist.
 int alloc_third(lsb_ctx* c, Rank& r) {
   const size_t per = (size_t)c->per;
-  int K = r.placement_k > 0 ? placement_candidates((double)per * sizeof(Elem), 3) : 1;
+  int K = r.placement_k > 0 ? placement_candidates((double)per * sizeof(Elem), 3) : 1;  // probed A and B only
   if (K <= 2) K = 1;
-  if (K == 1 || !r.os_status) return dev_alloc(&r.R, per);
+  if (K == 1 || !r.os_status) return rec_alloc(&r.R, per);
   std::vector<Elem*> cand;
   LSB_TRY(alloc_candidates(per, K, 1, cand));
   K = (int)cand.size();
@@ -264,13 +422,14 @@ int alloc_third(lsb_ctx* c, Rank& r) {
   }
   (void)hipFree(hist);
   if (rc == LSB_OK && pr.err != hipSuccess) rc = fail(LSB_ERR_HIP, "alloc_third: placement probe", hipGetErrorString(pr.err));
+  if (rc == LSB_OK && K > 1) rc = probe_check(r);
   if (rc != LSB_OK) {
-    for (Elem* p : cand) (void)hipFree(p);
+    for (Elem* p : cand) rec_free(p);
     return rc;
   }
   r.R = cand[bk];
   for (Elem* p : cand)
-    if (p != r.R) (void)hipFree(p);
+    if (p != r.R) rec_free(p);
   return LSB_OK;
 }
 
@@ -338,9 +497,9 @@ void free_rank(Rank& r) {
   (void)hipFree(r.os_ctr);
   (void)hipHostFree(r.os_err_h);
   (void)hipHostFree(r.os_hist_h);
-  (void)hipFree(r.A);
-  (void)hipFree(r.B);
-  (void)hipFree(r.R);
+  rec_free(r.A);
+  rec_free(r.B);
+  rec_free(r.R);
   (void)hipFree(r.chunk_hist);
   (void)hipFree(r.chunk_off);
   (void)hipFree(r.totals);

@@ -216,8 +216,8 @@ int exchange_loopback(lsb_ctx* c, int digit) {
   // digit-ordered A -> rank q's R.
   for (int j = 0; j < slices_of(c); ++j) {
     for (Rank& q : c->ranks) {
-      Timer t(c, &q, LSB_K_WIRE);
       HIP_TRY(hipSetDevice(q.dev));
+      Timer t(c, &q, LSB_K_WIRE);
       for (Rank& s : c->ranks) {
         if (s.rank == q.rank) continue;
         const int64_t cnt = s.send_counts[q.rank];
@@ -278,6 +278,20 @@ int peer_setup(lsb_ctx* c) {
   // One rank per process: IPC handles of both buffers, all-gathered.
   Rank& r = c->ranks[0];
   HIP_TRY(hipSetDevice(r.dev));
+  // IPC handles name hipMalloc memory only: a record buffer built from VMM
+  // pieces (rec_alloc) is replaced by a hipMalloc'd one holding its records.
+  for (int k = 0; k < 2; ++k) {
+    Elem* old = r.buf[k];
+    if (!rec_is_vmm(old)) continue;
+    Elem* nu = nullptr;
+    LSB_TRY(dev_alloc(&nu, (size_t)c->per));
+    HIP_TRY(hipMemcpyAsync(nu, old, sizeof(Elem) * (size_t)c->per, hipMemcpyDeviceToDevice, r.stream));
+    HIP_TRY(hipStreamSynchronize(r.stream));
+    for (Elem** p : {&r.A, &r.B, &r.R})
+      if (*p == old) *p = nu;
+    r.buf[k] = nu;
+    rec_free(old);
+  }
   static_assert(sizeof(hipIpcMemHandle_t) % 8 == 0, "handle in u64 words");
   constexpr size_t kW = sizeof(hipIpcMemHandle_t) / 8;  // words per handle
   std::vector<uint64_t> mine(2 * kW), all((size_t)P * 2 * kW);

@@ -1459,6 +1459,9 @@ struct PeerDests {
 };
 
 constexpr int kPeerBaseBlock = 1024;
+// s_waitcnt operand: vmcnt(0) (bits 3:0 and 15:14), expcnt(7) and lgkmcnt(15)
+// left at their maxima, i.e. wait for this wave's vector memory operations only.
+constexpr int kWaitVmcnt0 = 0x0F70;
 
 // One workgroup: base[b] for b < nb from the all-gathered counts hist[s * nb + b].
 __global__ __launch_bounds__(kPeerBaseBlock) void k_peer_base(const uint64_t* __restrict__ hist,
@@ -1527,12 +1530,19 @@ __global__ __launch_bounds__(kPlaceBlock) void k_peer_scatter(const Elem* __rest
     }
   }
   // Release at system scope (shmem_putmem's completion before
-  // shmem_barrier_all, shmem/shmem_lsbsort.cpp:455-456): after the barrier
-  // every wave's stores have left it (s_waitcnt), and one system-scope
-  // release per workgroup writes back this XCD's L2 (buffer_wbl2 sc0 sc1),
-  // so stores to a peer's memory that the L2 holds reach it before the
-  // kernel ends.  The owner acquires (k_system_acquire) after the barrier
-  // collective, before its next pass reads the buffer.
+  // shmem_barrier_all, shmem/shmem_lsbsort.cpp:455-456).  Every wave first
+  // waits for its own stores to complete (s_waitcnt vmcnt(0); a store
+  // completes once the L2 has taken it).  __syncthreads alone does not emit
+  // that wait: the compiler's workgroup-scope barrier relies on the CU's
+  // in-order path to the L2, which says nothing about what another wave's
+  // stores have reached when wave 0 writes the L2 back.  After the barrier
+  // the workgroup's stores are all in this XCD's L2, and one system-scope
+  // release writes it back (buffer_wbl2 sc0 sc1, then its own wait), so
+  // stores to a peer's memory that the L2 holds reach it before the kernel
+  // ends.  tests/test_peer_fence.py checks this order in the code object.
+  // The owner acquires (k_system_acquire) after the barrier collective,
+  // before its next pass reads the buffer.
+  __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
   __syncthreads();
   if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
 }

@@ -138,6 +138,7 @@ struct lsb_ctx {
   ncclComm_t comm = nullptr;
   lsb_comm_ops_t ops = {};  // Mode::kOps
   bool timing = false;
+  bool shared_device = false;  // two local ranks on one device (no placement probe)
   bool force_exchange = false;
   bool skip_constant = true;  // lsb_sort skips digits on which all keys agree
   int slices = 0;             // exchange slices (placement overlaps the next slice); 0 = default
@@ -158,7 +159,7 @@ struct lsb_ctx {
   uint64_t last_varying = 0;
   lsb::KeyGen keygen;
   std::vector<lsb_rt::PendingEvent> pending;
-  std::vector<hipEvent_t> event_pool;
+  std::vector<std::pair<int, hipEvent_t>> event_pool;  // (device, event) of finished timings
   int64_t launches[LSB_K_COUNT] = {};
   double total_ms[LSB_K_COUNT] = {};
   int64_t scatter_elems = 0;
@@ -265,6 +266,11 @@ int host_alloc(T** p, size_t count) {
 }
 
 // ---- context and rank buffers (lsb_context.cpp) -------------------------------
+// Record buffers (A, B, R, candidates): VMM-backed in 1 GiB pieces when at
+// least one piece long, else hipMalloc; rec_free frees either kind.
+int rec_alloc(Elem** p, size_t count);
+void rec_free(void* p);
+bool rec_is_vmm(const void* p);
 int max_chunks_for_device(int dev);
 int alloc_records(lsb_ctx* c, Rank& r);  // A and B (placement-calibrated)
 int alloc_third(lsb_ctx* c, Rank& r);    // R, placed against A and B

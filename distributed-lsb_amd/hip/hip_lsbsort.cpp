@@ -221,7 +221,8 @@ int run(World& w, const Options& o) {
   if (o.slices > 0) CHECK(lsb_set_option(w.ctx, LSB_OPT_EXCHANGE_SLICES, o.slices));
   if (o.hybrid > 0) CHECK(lsb_set_option(w.ctx, LSB_OPT_HYBRID, o.hybrid));
   if (w.root()) {
-    printf("Total number of HIP ranks: %d\n", w.P);
+    // the reference's own line (mpi/mpi_lsbsort.cpp:619): a rank here is one GPU
+    printf("Total number of MPI ranks: %d\n", w.P);
     printf("Problem size: %" PRId64 "\n", o.n);
     flush_output();
   }

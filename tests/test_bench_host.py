@@ -151,3 +151,51 @@ def test_eight_rank_dry_launch():
     assert x["link_bytes_per_exchange"] == {"max": 8 * mib, "min": mib}
     assert x["rank_bytes_per_sort"] == {"max": 7 * 4 * 8 * mib, "min": 7 * 4 * mib}
     assert x["link_bytes_per_sort"]["max_link"][0] == 7 and x["link_bytes_per_sort"]["max_over_min"] == 8.0
+
+
+# ---- N = 1: the extras after the headline -------------
+def test_one_gpu_line_carries_hybrid_x16_and_c5_keys():
+    """N = 1 runs two extras in fresh processes: the hybrid local sort and
+    x16, the reference's 16-bit digit (BASELINE configs[4]) with its exchange
+    path forced through a world-of-one RCCL communicator (--force-exchange);
+    both are priced against SURVEY 8(d)'s C5 denominator (192 B per record)."""
+    r = _bench(["--dry-rank", "--no-cpu-baseline", "--steps", "2"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = _line(r.stdout)
+    assert out["n_gpus"] == 1 and out["value"] == 8.0 and out["verified"] is True
+    assert out["hybrid_melem_s"] == 8.0 and out["hybrid_verified"] is True
+    assert out["x16_melem_s"] == 16.0 and out["x16_verified"] is True  # --radix-bits 16
+    x = out["x16_exchange_roofline"]
+    assert x["bound"] == "self" and x["peak"] is None and x["frac"] is None
+    mib = 1 << 20
+    assert x["link_bytes_per_exchange"] == {"max": mib, "min": mib} and x["exchanges_per_sort"] == 4
+    assert x["place"]["tail_ms_per_sort"] == 0.5 and x["place"]["ms_per_sort"] == 2.0
+    assert out["x16_per_pass"][0]["place_tail_ms"] == 0.125
+    frac = round(192 * (1 << 30) / 1e-3 / 8e12, 4)  # dry lines report 1 ms per step
+    assert out["hybrid_c5_survey_frac"] == frac and out["x16_c5_survey_frac"] == frac
+    assert "two stable 8-bit passes" in out["c5_basis"]
+
+
+def test_x16_failure_keeps_the_headline():
+    r = _bench(["--dry-rank", "--no-cpu-baseline", "--steps", "2", "--dry-fail-x16", "0"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = _line(r.stdout)
+    assert out["value"] == 8.0 and out["hybrid_melem_s"] == 8.0
+    assert "x16_melem_s" not in out and "rank exit codes" in out["x16_error"]
+
+
+@pytest.mark.parametrize("form", ["x16", "hybrid"])
+def test_wrong_extra_output_fails_the_run(form):
+    """An extra whose output fails lsb_verify fails the run (exit 1), as the
+    headline does, but its line is still printed (advisor r04)."""
+    r = _bench(["--dry-rank", "--no-cpu-baseline", "--steps", "2", "--dry-unverified", form])
+    assert r.returncode == 1
+    out = _line(r.stdout)
+    assert out["verified"] is True and out[f"{form}_verified"] is False
+
+
+def test_wrong_peer_output_fails_the_run():
+    r = _bench(["--gpus", "2", "--dry-rank", "--no-cpu-baseline", "--steps", "2", "--dry-unverified", "peer"])
+    assert r.returncode == 1
+    out = _line(r.stdout)
+    assert out["verified"] is True and out["peer_verified"] is False and out["whole_key_verified"] is True

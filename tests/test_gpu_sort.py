@@ -565,7 +565,7 @@ def test_harness_matches_reference_lines(lsb_built, ref_vectors, extra):
     out = subprocess.run([exe, "--n", "1000003", "--ranks", "4", "--print"] + extra, check=True,
                          capture_output=True, text=True, timeout=300).stdout
     lines = out.splitlines()
-    assert lines[0] == "Total number of HIP ranks: 4"
+    assert lines[0] == "Total number of MPI ranks: 4"
     assert lines[1] == "Problem size: 1000003"
     assert "Verifying" in lines and "Array is sorted" in lines
     assert any(l.startswith("That's ") and l.endswith(" M elements sorted / s") for l in lines)
@@ -710,7 +710,7 @@ def test_harness_rccl_ranks_share_gpu(lsb_built, ref_vectors, n, P, extra):
     # RCCL prints its own init banner (RCCL / HIP / ROCm versions, ...) to
     # stdout from rank 0 on some setups, before the harness's first line.
     lines = r.stdout.splitlines()
-    head = f"Total number of HIP ranks: {P}"
+    head = f"Total number of MPI ranks: {P}"
     assert head in lines, r.stdout[:2000]
     lines = lines[lines.index(head):]
     assert lines[1] == f"Problem size: {n}"
