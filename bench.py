@@ -390,7 +390,7 @@ def parallelism(N, radix, a):
                                                        "grouped Send/Recv") +
                 ", stable merge tree of the P runs")
     return (f"block partition over {N} GPUs; per exchange digit RCCL AllGather of counts + " +
-            {"alltoallv": "AllToAllv in 4 slices", "p2p": "grouped Send/Recv in 4 slices",
+            {"alltoallv": "AllToAllv in 5 halving slices", "p2p": "grouped Send/Recv in 5 halving slices",
              "peer": "direct peer stores (IPC)"}[a.exchange])
 
 
@@ -598,6 +598,23 @@ def extras_at(a, N):
     return out
 
 
+MI355X_HBM_BYTES = 288 * 10**9  # device memory of one MI355X (spec); --dry-rank's stand-in for lsb_device_memory
+
+
+def memory_keys(a, N, radix, device_total, ranks_per_device=1):
+    """Device memory of one rank (lsb_rank_footprint, host arithmetic) against
+    the device's: A, B, R, look-back rows and tables, plus the optional
+    placement probe's transient (LSB_PLACEMENT_CANDIDATES) while it runs."""
+    with_recv = N > 1 or a.force_exchange or a.passes == "hybrid"
+    fp = lsbsort.rank_footprint(a.n_per_gpu * N, N, radix, with_recv)
+    peak = ranks_per_device * (fp["bytes"] + fp["probe_bytes"])
+    return {"bytes": fp["bytes"], "probe_bytes": fp["probe_bytes"], "ranks_per_device": ranks_per_device,
+            "device_bytes": device_total, "peak_frac": round(peak / device_total, 4) if device_total else None,
+            "fits": bool(device_total) and peak <= device_total,
+            "basis": "lsb_rank_footprint: A, B" + (", R" if with_recv else "") + ", look-back rows, tables; "
+                     "probe_bytes = the placement probe's candidates beyond A and B (0: no probe)"}
+
+
 def any_unverified(out):
     """The headline or any extra form produced output that failed lsb_verify
     (an extra that failed to run is `<name>_error`, not a wrong answer)."""
@@ -688,7 +705,8 @@ def dry_run(a):
     out = {"metric": METRIC, "value": float(d.world * radix), "ms_per_step": 1.0,
            "verified": form != a.dry_unverified,
            "n_gpus": d.world, "max_rank": top, "radix_bits": radix, "exchange": a.exchange,
-           "config": {"n_total": a.n_per_gpu * d.world}}
+           "config": {"n_total": a.n_per_gpu * d.world},
+           "device_memory": memory_keys(a, d.world, radix, MI355X_HBM_BYTES)}
     if d.world > 1 or a.force_exchange:
         out["exchange_roofline"] = exchange_roofline(
             d.all_gather_obj({"stats": dry_stats(d.rank, d.world, a.steps)}), a.steps)
@@ -865,6 +883,8 @@ def main():
     placement = w.placement()
     last = w.last_sort()
     w.close()
+    mem = memory_keys(a, N, radix, lsbsort.device_memory(device)[1],
+                      max(1, N // max(1, visible_devices())) if N > 1 else 1)
     xroof = exchange_roofline(d.all_gather_obj({"stats": xstats}), a.steps) if N > 1 or a.force_exchange else None
 
     ms_per_step = total / a.steps * 1e3
@@ -966,10 +986,13 @@ def main():
             "sort": "the whole sort, per rank"},
         "exchange_bytes_per_step": xbytes // a.steps if N > 1 or a.force_exchange else 0,
         "exchange_roofline": xroof,
-        "placement": dict(placement, basis="rank 0's A and B, chosen at context creation among `candidates` "
-                                            "buffers by one timed k_onesweep pass between every ordered pair; ms "
-                                            "per pass, mean of both directions: the kept pair, the first two "
-                                            "allocated, the slowest (lsb_get_placement; DESIGN.md 4)"),
+        "placement": dict(placement, record_alloc=os.environ.get("LSB_RECORD_ALLOC", "vmm 1 GiB pieces"),
+                          basis="rank 0's A and B: built from 1 GiB VMM pieces (no probe: candidates 0); with "
+                                "LSB_PLACEMENT_CANDIDATES = K > 2, chosen at context creation among K buffers "
+                                "by one timed k_onesweep pass between every ordered pair; ms per pass, mean "
+                                "of both directions: the kept pair, the first two allocated, the slowest "
+                                "(lsb_get_placement; DESIGN.md 4)"),
+        "device_memory": mem,
         "verified": verified,
         "vs_baseline_basis": "MPI mpi_lsbsort 830 M elem/s (64 nodes x 128 cores, n=2^36; BASELINE.md §1)",
         "library": lsbsort.build_info(),

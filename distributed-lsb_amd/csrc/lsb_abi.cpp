@@ -58,6 +58,48 @@ int lsb_create(lsb_ctx_t** out, int64_t n_total, int num_ranks, const int* dev_i
   return LSB_OK;
 }
 
+int lsb_rank_footprint(int64_t n_total, int num_ranks, int radix_bits, int with_recv, int64_t* bytes,
+                       int64_t* probe_bytes) {
+  if (!bytes || n_total < 0 || num_ranks < 1 || num_ranks > 64)
+    return fail(LSB_ERR_INVALID, "lsb_rank_footprint", "n, P or null");
+  if (radix_bits != 8 && radix_bits != 16 && radix_bits != 64)
+    return fail(LSB_ERR_UNSUPPORTED, "lsb_rank_footprint", "radix_bits must be 8, 16 or 64");
+  const int64_t P = num_ranks, per = div_ceil(n_total, num_ranks);
+  const int64_t nb = radix_bits == 64 ? lsb::kBuckets : (int64_t)1 << radix_bits;
+  const int64_t rec = rec_bytes((size_t)per);
+  const int64_t tiles = lsb::onesweep_tiles(per);
+  const lsb::Chunking ch = lsb::make_chunking(per, 2 * 256);
+  int64_t b = 2 * rec + (with_recv ? rec : 0);
+  b += tiles * lsb::kBuckets * 4;                                   // os_status
+  if (P > 1 || with_recv) b += tiles * (int64_t)sizeof(lsb::TileDesc) + 2 * P * nb * 8;  // gdesc, gstart
+  b += (int64_t)lsb::kBuckets * std::max(1, ch.num_chunks) * 12;    // chunk_hist, chunk_off
+  b += (int64_t)lsb::kBuckets * 8 + (radix_bits == 16 ? 2 * 65536 * 8 : 0);  // totals, totals16, first16
+  b += (std::max(P * nb, 4 * P) + (P * nb + P) + P * nb + nb + 2 * P) * 8;   // gather, place, plan_*
+  b += (2 * lsb::kOnesweepSubs * lsb::kBuckets + 2 * lsb::kOnesweepSubs) * 4 +
+       (int64_t)lsb::kOnesweepSubs * lsb::kBuckets * 8;             // os_hist, os_ctr, seg_base
+  if (radix_bits == 64 && P > 1)
+    b += (lsb::merge_tiles(per) + 2 * lsb::kMergeMaxPairs + 1) * 8 +
+         (int64_t)(P * 8) * lsb::kSplitCands * 8 * (P + 1);         // merge_path, split_* (8 slices)
+  *bytes = b;
+  if (probe_bytes) {
+    int K = 0;
+    if (const char* e = getenv("LSB_PLACEMENT_CANDIDATES")) K = atoi(e);
+    K = std::min(K, 8);
+    *probe_bytes = K > 2 && rec >= ((int64_t)1 << 30) ? (K - 2) * rec : 0;
+  }
+  return LSB_OK;
+}
+
+int lsb_device_memory(int dev, int64_t* free_bytes, int64_t* total_bytes) {
+  if (!free_bytes || !total_bytes) return fail(LSB_ERR_INVALID, "lsb_device_memory", "null");
+  HIP_TRY(hipSetDevice(dev));
+  size_t f = 0, t = 0;
+  HIP_TRY(hipMemGetInfo(&f, &t));
+  *free_bytes = (int64_t)f;
+  *total_bytes = (int64_t)t;
+  return LSB_OK;
+}
+
 int lsb_device_count(int* count) {
   if (!count) return fail(LSB_ERR_INVALID, "lsb_device_count", "null");
   *count = 0;

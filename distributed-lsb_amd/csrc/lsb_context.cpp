@@ -124,6 +124,12 @@ void vmm_release(VmmBuffer& b, size_t piece) {
 
 }  // namespace
 
+size_t rec_bytes(size_t count) {
+  const size_t piece = vmm_piece_bytes();
+  const size_t want = std::max<size_t>(count, 1) * sizeof(Elem);
+  return piece == 0 || want < piece ? want : (want + piece - 1) / piece * piece;
+}
+
 bool rec_is_vmm(const void* p) {
   std::lock_guard<std::mutex> lock(g_vmm_mu);
   for (const VmmBuffer& b : g_vmm)

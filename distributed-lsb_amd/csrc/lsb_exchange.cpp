@@ -174,8 +174,8 @@ int place_slice(lsb_ctx* c, Rank& r, int shift, int j) {
   const bool self_in_r = c->self_coll && c->mode != Mode::kLoopback;
   for (int s = 0; s < c->P; ++s) {
     if (s == r.rank && !self_in_r) continue;
-    const int64_t lo = part(r.recv_counts[s], j, slices_of(c));
-    const int64_t hi = part(r.recv_counts[s], j + 1, slices_of(c));
+    const int64_t lo = slice_part(r.recv_counts[s], j, slices_of(c));
+    const int64_t hi = slice_part(r.recv_counts[s], j + 1, slices_of(c));
     LSB_TRY(place_range(c, r, shift, s, r.R + r.recv_displs[s] + lo, r.recv_displs[s] + lo, hi - lo));
   }
   return LSB_OK;
@@ -221,7 +221,7 @@ int exchange_loopback(lsb_ctx* c, int digit) {
       for (Rank& s : c->ranks) {
         if (s.rank == q.rank) continue;
         const int64_t cnt = s.send_counts[q.rank];
-        const int64_t lo = part(cnt, j, slices_of(c)), hi = part(cnt, j + 1, slices_of(c));
+        const int64_t lo = slice_part(cnt, j, slices_of(c)), hi = slice_part(cnt, j + 1, slices_of(c));
         if (hi <= lo) continue;
         HIP_TRY(hipMemcpyAsync(q.R + q.recv_displs[s.rank] + lo, s.A + s.send_displs[q.rank] + lo,
                                (size_t)(hi - lo) * sizeof(Elem), hipMemcpyDefault, q.stream));
@@ -420,10 +420,10 @@ int exchange_rccl(lsb_ctx* c, int digit) {
     {
       Timer t(c, &r, LSB_K_WIRE);
       for (int q = 0; q < P; ++q) {
-        const int64_t slo = part(r.send_counts[q], j, slices_of(c));
-        const int64_t shi = part(r.send_counts[q], j + 1, slices_of(c));
-        const int64_t rlo = part(r.recv_counts[q], j, slices_of(c));
-        const int64_t rhi = part(r.recv_counts[q], j + 1, slices_of(c));
+        const int64_t slo = slice_part(r.send_counts[q], j, slices_of(c));
+        const int64_t shi = slice_part(r.send_counts[q], j + 1, slices_of(c));
+        const int64_t rlo = slice_part(r.recv_counts[q], j, slices_of(c));
+        const int64_t rhi = slice_part(r.recv_counts[q], j + 1, slices_of(c));
         sc[q] = q == me && skip_self ? 0 : (size_t)(shi - slo) * 2;
         rc[q] = q == me && skip_self ? 0 : (size_t)(rhi - rlo) * 2;
         sd[q] = (size_t)(r.send_displs[q] + slo) * 2;

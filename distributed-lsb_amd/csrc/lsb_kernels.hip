@@ -762,8 +762,10 @@ __device__ unsigned long long g_os_prof[10];
 // throughout, and its bucket-b run adds cnt_b to count16[b][lo]; thread b
 // keeps a running count per (b, lo) in registers and adds it to memory when
 // its tile's low byte changes (a workgroup's tiles are taken in order, so
-// that is a few times per launch).  A tile across a low-byte boundary walks
-// its staged runs.
+// that is a few times per launch).  A tile across a low-byte boundary adds
+// its counts in the write-out instead: each wave-instruction's run of equal
+// (digit, low byte) slots adds once, from its head lane (run-length atomics,
+// so a hot key's run costs one add per instruction, not one per record).
 //
 // HALVES = 2 (skewed keys, chosen per sort by the runtime): the ranked tile
 // is staged and written in two halves of the tile's output order, so the

@@ -269,6 +269,7 @@ int host_alloc(T** p, size_t count) {
 // Record buffers (A, B, R, candidates): VMM-backed in 1 GiB pieces when at
 // least one piece long, else hipMalloc; rec_free frees either kind.
 int rec_alloc(Elem** p, size_t count);
+size_t rec_bytes(size_t count);  // device bytes rec_alloc takes for count records
 void rec_free(void* p);
 bool rec_is_vmm(const void* p);
 int max_chunks_for_device(int dev);
@@ -331,15 +332,27 @@ void os_profile_report();
 // ---- per-digit exchange (lsb_exchange.cpp) ------------------------------------
 
 // ---- placement, overlapped with the exchange ------------------------------
-// Part j of n records cut into `slices` parts: [part(n, j), part(n, j + 1)).
-// Sender and receiver cut a segment alike (send_counts[q] at s equals
-// recv_counts[s] at q).
+// Part j of n records cut into `slices` equal parts: [part(n, j), part(n, j + 1))
+// (the whole-key exchange's owner slices).
 inline int64_t part(int64_t n, int j, int slices) { return n * j / slices; }
 
-// Slices of an exchange: the option, else 4 per exchange digit, or 8 for the
-// whole-key exchange, whose one all-to-all carries every record: its last
-// slice's merge (ceil(log2 P) levels) is the tail after the wire goes quiet.
-inline int slices_of(const lsb_ctx* c) { return c->slices > 0 ? c->slices : (c->bits == 64 ? 8 : 4); }
+// Part j of a per-digit exchange segment of n records cut into `slices`
+// halving parts: n/2, n/4, ..., and the last two n / 2^(slices-1) each.  A
+// slice is placed (or counted) while the next one is on the wire, so what
+// runs after the wire goes quiet is the last slice's placement: 1/16 of the
+// records at 5 slices where equal slices leave 1/4 at 4.
+// Sender and receiver cut a segment alike (send_counts[q] at s equals
+// recv_counts[s] at q).
+inline int64_t slice_part(int64_t n, int j, int slices) {
+  if (j >= slices) return n;
+  return j >= 63 ? n : n - (n >> j);
+}
+
+// Slices of an exchange: the option, else 5 halving slices per exchange digit,
+// or 8 equal slices for the whole-key exchange, whose one all-to-all carries
+// every record: its last slice's merge (ceil(log2 P) levels) is the tail
+// after the wire goes quiet.
+inline int slices_of(const lsb_ctx* c) { return c->slices > 0 ? c->slices : (c->bits == 64 ? 8 : 5); }
 int ensure_recv(lsb_ctx* c, Rank& r);
 int join_place(Rank& r);
 int join_place_timed(lsb_ctx* c, Rank& r);

@@ -180,6 +180,8 @@ def _lib() -> ctypes.CDLL:
             "lsb_get_pass_exchange": (i32, [vp, i32, P64, ctypes.POINTER(ctypes.c_double),
                                             ctypes.POINTER(ctypes.c_double)]),
             "lsb_build_info": (cp, []),
+            "lsb_rank_footprint": (i32, [i64, i32, i32, i32, P64, P64]),
+            "lsb_device_memory": (i32, [i32, P64, P64]),
             "lsb_plan_exchange": (i32, [i64, i32, i32, i32, vp, vp, vp, vp, vp, vp]),
             "lsb_plan_exchange_device": (i32, [i32, i64, i32, i32, i32, vp, vp, vp, vp, vp, vp]),
             "lsb_plan_merge": (i32, [i64, i32, i32, vp, vp, vp, vp, vp, vp]),
@@ -204,6 +206,24 @@ def per_rank(n: int, P: int) -> int:
 
 def here(n: int, P: int, r: int) -> int:
     return int(_lib().lsb_here(n, P, r))
+
+
+def rank_footprint(n: int, P: int, radix_bits: int = 8, with_recv: bool = False) -> dict:
+    """lsb_rank_footprint: device bytes one rank of lsb_create(n, P, radix_bits)
+    holds ({"bytes"}), and the optional placement probe's transient on top
+    ({"probe_bytes"}, from LSB_PLACEMENT_CANDIDATES as set now).  Host
+    arithmetic only."""
+    b, pb = ctypes.c_int64(), ctypes.c_int64()
+    _check(_lib().lsb_rank_footprint(n, P, radix_bits, int(with_recv), ctypes.byref(b), ctypes.byref(pb)),
+           "lsb_rank_footprint")
+    return {"bytes": b.value, "probe_bytes": pb.value}
+
+
+def device_memory(dev: int = 0) -> tuple:
+    """(free, total) device bytes of device dev (lsb_device_memory)."""
+    f, t = ctypes.c_int64(), ctypes.c_int64()
+    _check(_lib().lsb_device_memory(dev, ctypes.byref(f), ctypes.byref(t)), "lsb_device_memory")
+    return f.value, t.value
 
 
 def build_info() -> dict:

@@ -78,9 +78,12 @@ typedef struct lsb_ctx lsb_ctx_t;
 #define LSB_OPT_FORCE_EXCHANGE  1  /* 1: run the exchange path even when P == 1 */
 #define LSB_OPT_SKIP_CONSTANT_DIGITS 2  /* 1 (default): lsb_sort skips every digit after
                                            the first on which all keys agree */
-#define LSB_OPT_EXCHANGE_SLICES 3  /* 1..64 (default 4; 8 for radix_bits = 64): the all-to-all of a pass is cut into
+#define LSB_OPT_EXCHANGE_SLICES 3  /* 1..64 (default 5; 8 for radix_bits = 64): the all-to-all of a pass is cut into
                                       this many groups; each slice is placed while the next
-                                      is in flight */
+                                      is in flight.  Per-digit exchanges cut each peer segment
+                                      in halving parts (1/2, 1/4, ..., the last two equal), so
+                                      the placement left after the wire is 1/2^(slices-1) of it;
+                                      the whole-key exchange in equal parts */
 #define LSB_OPT_EXCHANGE_P2P    4  /* RCCL contexts: 0 (default) ncclAllToAllv per slice,
                                       1 the same as grouped ncclSend/ncclRecv */
 #define LSB_OPT_EXCHANGE_PEER   5  /* 1: exchange by direct stores into the owners' buffers
@@ -300,17 +303,39 @@ int  lsb_get_exchange_stats(lsb_ctx_t* ctx, lsb_exchange_stats_t* out);
 int  lsb_get_pass_exchange(lsb_ctx_t* ctx, int pass, int64_t* bytes, double* wire_ms,
                            double* place_tail_ms);
 
-/* How the local rank's record buffers A and B were placed: at creation a rank
- * whose buffers hold >= 1 GiB allocates `candidates` buffers (environment
- * LSB_PLACEMENT_CANDIDATES, default 8, as many as fit; 0 here: A and B as
- * allocated), times one k_onesweep pass over uniform keys between every
- * ordered pair, keeps the pair fastest both ways and frees the rest (the pass
- * runs up to ~8 % slower between some pairs than others, with where the driver
- * puts a 16 GiB buffer).  Milliseconds per pass, mean of both
- * directions: the chosen pair, the first two buffers allocated (what a plain
- * allocation would have kept) and the slowest pair. */
+/* How the local rank's record buffers A and B were placed.  Record buffers of
+ * at least 1 GiB are built from 1 GiB physical pieces (HIP virtual memory;
+ * LSB_RECORD_ALLOC=malloc: hipMalloc), which run every pass at the same speed
+ * in every process.  The round-4 placement probe remains as an
+ * option: with LSB_PLACEMENT_CANDIDATES = K > 2 (at most 8) a rank whose
+ * buffers hold >= 1 GiB and that shares its device with no other rank of the
+ * context allocates K candidate buffers (as many as fit in 90 % of the free
+ * memory; a transient peak of K record buffers, see lsb_rank_footprint),
+ * times one k_onesweep pass over uniform keys between every ordered pair,
+ * keeps the pair fastest both ways and frees the rest.  candidates = 0: no
+ * probe ran.  Milliseconds per pass, mean of both directions: the chosen
+ * pair, the first two buffers allocated (what a plain allocation would have
+ * kept) and the slowest pair. */
 int  lsb_get_placement(lsb_ctx_t* ctx, int rank, int* candidates, double* chosen_ms,
                        double* first_pair_ms, double* worst_ms);
+
+/* ---- device memory ------------------------------------------------------ */
+/* Device bytes one rank of a context lsb_create(n_total, num_ranks,
+ * radix_bits) holds (pure host arithmetic, no device needed): A and B (each
+ * `per` records, rounded up to whole 1 GiB pieces when built from them), the
+ * receive buffer R when with_recv (any exchange: num_ranks > 1 or forced; the
+ * hybrid local sort), the single-read passes' look-back rows (4 B per bucket
+ * per 4096-record tile), the gathered passes' tile descriptors (exchanges),
+ * and the count and plan tables.  *probe_bytes: what the optional placement
+ * probe (LSB_PLACEMENT_CANDIDATES, read from the environment now) holds on
+ * top while it runs, at most; 0 when no probe would run.  A model of
+ * init_rank's allocations, checked against the device's own free-memory
+ * count by tests/test_footprint_gpu.py. */
+int  lsb_rank_footprint(int64_t n_total, int num_ranks, int radix_bits, int with_recv,
+                        int64_t* bytes, int64_t* probe_bytes);
+
+/* Free and total device memory of device dev (hipMemGetInfo). */
+int  lsb_device_memory(int dev, int64_t* free_bytes, int64_t* total_bytes);
 
 /* ---- build --------------------------------------------------------------- */
 /* "sha256=<digest of the sources the library was built from> host=<build

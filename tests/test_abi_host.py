@@ -337,3 +337,33 @@ def test_plan_merge_rejects_bad_counts(lsb_built):
         lsb_built.plan_merge(n, P, 0, np.array([[30], [30]]), np.array([[20], [40]]))
     with pytest.raises(lsb_built.LsbError):      # more than the rank holds
         lsb_built.plan_merge(n, P, 0, np.array([[40], [9]]), np.array([[60], [10]]))
+
+
+def test_rank_footprint_model(lsb_built, monkeypatch):
+    """lsb_rank_footprint (host arithmetic): record buffers rounded up to whole
+    1 GiB VMM pieces (hipMalloc'd ones are not), R only with an exchange or
+    the hybrid, 4 B of look-back row per bucket per 4096-record tile, and the
+    placement probe's K - 2 extra candidates only when asked for."""
+    L = lsb_built
+    gib = 1 << 30
+    monkeypatch.delenv("LSB_PLACEMENT_CANDIDATES", raising=False)
+    monkeypatch.delenv("LSB_RECORD_ALLOC", raising=False)
+    monkeypatch.delenv("LSB_VMM_CHUNK_MIB", raising=False)
+    n = 1 << 30
+    rows = (n // 4096) * 256 * 4
+    f = L.rank_footprint(n, 1, 8)
+    assert f["probe_bytes"] == 0 and 0 <= f["bytes"] - 32 * gib - rows < 64 << 20
+    extra = L.rank_footprint(n, 1, 8, with_recv=True)["bytes"] - f["bytes"]
+    assert 16 * gib <= extra < 16 * gib + (64 << 20)  # R, and the gathered passes' tile descriptors
+    ragged = L.rank_footprint(n + 12345, 1, 8)["bytes"]
+    assert ragged - f["bytes"] >= 2 * gib  # A and B each take a 17th piece
+    monkeypatch.setenv("LSB_RECORD_ALLOC", "malloc")
+    assert L.rank_footprint(n + 12345, 1, 8)["bytes"] - f["bytes"] < 1 << 20
+    monkeypatch.delenv("LSB_RECORD_ALLOC")
+    monkeypatch.setenv("LSB_PLACEMENT_CANDIDATES", "8")
+    assert L.rank_footprint(n, 1, 8)["probe_bytes"] == 6 * 16 * gib
+    assert L.rank_footprint(1 << 20, 1, 8)["probe_bytes"] == 0  # buffers under 1 GiB: no probe
+    # P ranks: per = ceil(n / P) records each
+    assert L.rank_footprint(8 * n, 8, 16, with_recv=True)["bytes"] > 48 * gib
+    with pytest.raises(L.LsbError):
+        L.rank_footprint(n, 0, 8)

@@ -199,3 +199,26 @@ def test_wrong_peer_output_fails_the_run():
     assert r.returncode == 1
     out = _line(r.stdout)
     assert out["verified"] is True and out["peer_verified"] is False and out["whole_key_verified"] is True
+
+
+@pytest.mark.parametrize("candidates", [None, "8"])
+def test_eight_rank_memory_fits_the_device(candidates):
+    """at the driver's N = 8 (2^30 records per GPU) one
+    rank's A, B, R, look-back rows and tables fit one MI355X (288 GB, the
+    dry run's stand-in for lsb_device_memory), also with the optional
+    placement probe's 8 candidates (LSB_PLACEMENT_CANDIDATES=8), and a
+    failing peer extra keeps the headline line."""
+    env = dict(os.environ)
+    env.pop("LSB_PLACEMENT_CANDIDATES", None)
+    if candidates:
+        env["LSB_PLACEMENT_CANDIDATES"] = candidates
+    r = _bench(["--gpus", "8", "--dry-rank", "--no-cpu-baseline", "--steps", "2", "--warmup", "1",
+                "--dry-fail-peer", "5", "--no-whole-key"], env=env, timeout=420)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = _line(r.stdout)
+    assert out["value"] == 8 * 16 and "rank exit codes" in out["peer_error"]
+    m = out["device_memory"]
+    gib = 1 << 30
+    assert 48 * gib <= m["bytes"] < 49 * gib  # A, B, R of 16 GiB each + 1/64 look-back rows
+    assert m["probe_bytes"] == (6 * 16 * gib if candidates else 0)
+    assert m["device_bytes"] == 288 * 10**9 and m["fits"] and m["peak_frac"] < 0.9

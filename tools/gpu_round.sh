@@ -106,7 +106,7 @@ for s in $RUN; do
       tail -12 $O/rot.log ;;
     clock)  # effective GPU clock per k_onesweep launch: GRBM_GUI_ACTIVE cycles / launch ns (warming box)
       (cd /tmp && TMPDIR=/tmp timeout -k 10 300 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE GRBM_COUNT \
-        --kernel-include-regex k_onesweep --output-format csv -d $O/clock -o run -- \
+        --kernel-include-regex 'k_onesweep<' --output-format csv -d $O/clock -o run -- \
         python3 $R/bench.py --steps 8 --warmup 2 --no-cpu-baseline --no-traffic --no-extras) > $O/clock.log 2>&1 \
         || fail clock $O/clock.log
       python3 tools/clock_summary.py $O/clock | tail -20 ;;

@@ -1,0 +1,33 @@
+#!/bin/bash
+# Counters behind the record-buffer allocation: the sort
+# of 2^30 records (tools/alloc_probe.py, one context, 2 sorts) in fresh
+# processes, hipMalloc'd buffers (LSB_RECORD_ALLOC=malloc, several processes:
+# the driver's placement varies) against 1 GiB VMM pieces, one counter set
+# per process (UTCL1 translation; L2 -> fabric requests), each process's own
+# per-pass times beside its counters.
+# Output: gpurun_out/r05_allocpmc/<mode>_<set>/ (csv) and .log; avail.txt.
+set -uo pipefail
+REPO=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$REPO/gpurun_out/${TAG:-r05_allocpmc}
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+timeout -s KILL 60 rocprofv3 -L > "$OUT/avail.txt" 2>&1 || true
+utcl="TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_PERMISSION_MISS_sum TCP_UTCL1_REQUEST_sum"
+tcc="TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_STALL_sum"
+run() {  # name alloc set
+  local name=$1 alloc=$2 set=$3 C
+  [ "$set" = utcl ] && C=$utcl || C=$tcc
+  LSB_RECORD_ALLOC=$alloc timeout -s KILL 150 rocprofv3 --kernel-trace --pmc $C --output-format csv \
+    -d "$OUT/${name}_$set" -o run -- python3 $REPO/tools/alloc_probe.py 30 1 2 > "$OUT/${name}_$set.log" 2>&1
+  local rc=$?
+  echo "$name $set rc=$rc $(grep -h '"passes"' "$OUT/${name}_$set.log" | tail -1)"
+  return $rc
+}
+for i in 1 2 3; do
+  run malloc$i malloc utcl || exit 1
+  run malloc$i malloc tcc || exit 1
+done
+for i in 1 2; do
+  run vmm$i vmm utcl || exit 1
+  run vmm$i vmm tcc || exit 1
+done
