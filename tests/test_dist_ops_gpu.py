@@ -38,6 +38,7 @@ def _worker(rank, world, port, case, result_dir):
     import lsbsort
     from bench import GlooComm  # lsb_comm_ops_t over gloo (bench.py --transport gloo)
 
+    os.environ.update(case.get("env", {}))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     n, bits, slices, mask = case["n"], case["bits"], case["slices"], case["mask"]
     w = lsbsort.World.rank_ops(n, world, rank, 0, GlooComm(dist, world, rank), radix_bits=bits)
@@ -84,11 +85,15 @@ def test_processes_reproduce_reference_digest(tmp_path, digests, oracle_mod, wor
         assert m[4] == 64 // bits                       # one exchange per digit
 
 
-@pytest.mark.parametrize("world,bits", [(2, 8), (4, 16)])
-def test_processes_peer_store_exchange(tmp_path, digests, oracle_mod, world, bits):
-    """Peer stores through IPC-mapped buffers of the other processes."""
+@pytest.mark.parametrize("world,bits,vmm_mib", [(2, 8, 0), (4, 16, 0), (2, 16, 2), (4, 8, 2)])
+def test_processes_peer_store_exchange(tmp_path, digests, oracle_mod, world, bits, vmm_mib):
+    """Peer stores through IPC-mapped buffers of the other processes.  With
+    vmm_mib, the record buffers start as VMM pieces of that many MiB, which
+    IPC handles cannot name: the exchange's setup moves them into hipMalloc
+    buffers first (peer_setup), records and all."""
     row = next(r for r in digests["rows"] if r["P"] == world)
-    out, meta = _run(tmp_path, world, dict(n=row["n"], bits=bits, slices=4, mask=None, peer=1))
+    env = {"LSB_VMM_CHUNK_MIB": str(vmm_mib)} if vmm_mib else {}
+    out, meta = _run(tmp_path, world, dict(n=row["n"], bits=bits, slices=4, mask=None, peer=1, env=env))
     assert oracle_mod.digest(out) == row["output"]
     for m in meta:
         assert m[0] == 1 and m[1] == -1 and m[2] == 1

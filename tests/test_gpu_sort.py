@@ -719,13 +719,34 @@ def test_harness_rccl_ranks_share_gpu(lsb_built, ref_vectors, n, P, extra):
     assert printed == [f"A[{i}] = ({k},{v})" for i, k, v in case["input"] + case["output"]]
 
 
-# ------------------------------------------ placement-calibrated A and B
-def test_placement_calibrated_buffers(lsb_built, monkeypatch):
-    """A rank whose record buffers hold >= 1 GiB picks A and B among 8
-    candidate buffers by a timed pass (lsb_get_placement); with
-    LSB_PLACEMENT_CANDIDATES=2 it keeps the first two allocated.  Either way
-    the sort is the same (verified on device)."""
-    n = 1 << 26  # 1 GiB per buffer
+# ------------------------------------- record buffers and the opt-in probe
+@pytest.mark.parametrize("alloc", ["vmm", "malloc"])
+def test_record_buffers_and_opt_in_probe(lsb_built, monkeypatch, alloc):
+    """Record buffers of >= 1 GiB are built from 1 GiB VMM pieces
+    (LSB_RECORD_ALLOC=malloc: hipMalloc) and no placement probe runs by
+    default (lsb_get_placement: 0 candidates).  LSB_PLACEMENT_CANDIDATES=8
+    still picks A and B among 8 candidate buffers by a timed pass, and R
+    among 3.  Every form sorts the same (verified on device), the local LSD
+    passes, the hybrid (R) and the forced exchange (R)."""
+    monkeypatch.delenv("LSB_PLACEMENT_CANDIDATES", raising=False)
+    if alloc == "malloc":
+        monkeypatch.setenv("LSB_RECORD_ALLOC", "malloc")
+    n = (1 << 26) + 4097  # 1 GiB and a tile per buffer: two pieces, the second nearly empty
+    with lsb_built.World(n, ranks=1) as w:
+        assert w.placement()["candidates"] == 0
+        w.generate()
+        w.my_sort()
+        assert w.verify() == (True, -1)
+        w.set_option(lsb_built.OPT_HYBRID, 1)
+        w.generate()
+        w.my_sort()
+        assert w.verify() == (True, -1)
+    with lsb_built.World(n, ranks=1, radix_bits=16) as w:  # R of the exchange path
+        w.set_option(lsb_built.OPT_FORCE_EXCHANGE, 1)
+        w.generate()
+        w.my_sort()
+        assert w.verify() == (True, -1)
+    monkeypatch.setenv("LSB_PLACEMENT_CANDIDATES", "8")
     with lsb_built.World(n, ranks=1) as w:
         p = w.placement()
         assert p["candidates"] == 8, p
@@ -739,11 +760,6 @@ def test_placement_calibrated_buffers(lsb_built, monkeypatch):
         w.generate()
         w.my_sort()
         assert w.verify() == (True, -1)
-    with lsb_built.World(n, ranks=1, radix_bits=16) as w:  # R of the exchange path
-        w.set_option(lsb_built.OPT_FORCE_EXCHANGE, 1)
-        w.generate()
-        w.my_sort()
-        assert w.verify() == (True, -1)
     monkeypatch.setenv("LSB_PLACEMENT_PICK", "worst")  # the experiment hook keeps the slowest pair
     with lsb_built.World(n, ranks=1) as w:
         p = w.placement()
@@ -752,11 +768,25 @@ def test_placement_calibrated_buffers(lsb_built, monkeypatch):
         w.my_sort()
         assert w.verify() == (True, -1)
     monkeypatch.delenv("LSB_PLACEMENT_PICK")
-    monkeypatch.setenv("LSB_PLACEMENT_CANDIDATES", "2")
-    with lsb_built.World(n, ranks=1) as w:
-        assert w.placement()["candidates"] == 0
+    # P logical ranks on one device never probe (the advisor's shared-device case)
+    with lsb_built.World(4 * n, ranks=4) as w:
+        assert all(w.placement(r)["candidates"] == 0 for r in range(4))
+
+
+@pytest.mark.parametrize("P,bits,hybrid", [(1, 8, 0), (1, 8, 1), (2, 16, 0), (8, 8, 0), (8, 16, 0), (4, 64, 0)])
+def test_small_vmm_pieces_golden(lsb_built, oracle_mod, digests, monkeypatch, P, bits, hybrid):
+    """Every record buffer built from 2 MiB VMM pieces (LSB_VMM_CHUNK_MIB=2),
+    so the small golden cases run the VMM allocator, with several pieces per
+    buffer, through every form: LSD passes, the hybrid, the per-digit and
+    whole-key exchanges between logical ranks (device copies between VMM
+    buffers)."""
+    monkeypatch.setenv("LSB_VMM_CHUNK_MIB", "2")
+    row = next(r for r in digests["rows"] if r["P"] == P)
+    with lsb_built.World(row["n"], ranks=P, radix_bits=bits) as w:
+        w.set_option(lsb_built.OPT_HYBRID, hybrid)
         w.generate()
         w.my_sort()
+        assert oracle_mod.digest(w.gather_global()) == row["output"]
         assert w.verify() == (True, -1)
     with lsb_built.World(1 << 20, ranks=1) as w:  # small buffers: as allocated
         assert w.placement() == {"candidates": 0, "chosen_ms": 0.0, "first_pair_ms": 0.0, "worst_ms": 0.0}
