@@ -558,9 +558,34 @@ int coll_allgather_u64(lsb_ctx* c, Rank& r, const uint64_t* send, uint64_t* recv
 }
 
 // MPI_Alltoallv semantics in uint64 units (counts and displacements).
+// `bound`: a count no rank sends to any peer in this call exceeds (the same on
+// every rank: every rank must issue the same RCCL calls).  RCCL moves a
+// per-peer range of 2 GiB or more wrongly (the world-of-one exchange at 2^28
+// records per rank, 2 GiB in its first slice, verified false; 512 MiB per
+// call verified: profiles/r05/x16dbg_probe.log), so an RCCL call whose bound
+// exceeds kMaxCallU64 goes as ceil(bound / kMaxCallU64) calls, call i
+// carrying part i of every peer's range on both sides.  (The reference's
+// MPI_Alltoallv takes int counts and cannot pass 2^31 records at all,
+// mpi/mpi_lsbsort.cpp:292-313.)
 int coll_alltoallv_u64(lsb_ctx* c, Rank& r, const uint64_t* send, const size_t* sc,
-                       const size_t* sd, uint64_t* recv, const size_t* rc, const size_t* rd) {
+                       const size_t* sd, uint64_t* recv, const size_t* rc, const size_t* rd,
+                       size_t bound) {
   const int P = c->P;
+  const size_t k = c->mode == Mode::kRccl ? std::max<size_t>(1, (bound + kMaxCallU64 - 1) / kMaxCallU64) : 1;
+  if (k > 1) {
+    std::vector<size_t> sc1(P), sd1(P), rc1(P), rd1(P);
+    auto cut = [&](size_t n, size_t i) { return (size_t)((unsigned __int128)n * i / k); };
+    for (size_t i = 0; i < k; ++i) {
+      for (int q = 0; q < P; ++q) {
+        sd1[q] = sd[q] + cut(sc[q], i);
+        sc1[q] = cut(sc[q], i + 1) - cut(sc[q], i);
+        rd1[q] = rd[q] + cut(rc[q], i);
+        rc1[q] = cut(rc[q], i + 1) - cut(rc[q], i);
+      }
+      LSB_TRY(coll_alltoallv_u64(c, r, send, sc1.data(), sd1.data(), recv, rc1.data(), rd1.data(), 0));
+    }
+    return LSB_OK;
+  }
   int64_t call_bytes = 0;
   for (int q = 0; q < P; ++q) call_bytes += (int64_t)sc[q] * 8;
   c->coll_calls += 1;

@@ -431,7 +431,7 @@ int exchange_rccl(lsb_ctx* c, int digit) {
       }
       LSB_TRY(coll_alltoallv_u64(c, r, reinterpret_cast<const uint64_t*>(r.A), sc.data(),
                                  sd.data(), reinterpret_cast<uint64_t*>(r.R), rc.data(),
-                                 rdp.data()));
+                                 rdp.data(), (size_t)slice_bound(c->per, j, slices_of(c)) * 2));
     }
     LSB_TRY(place_slice(c, r, shift, j));
   }

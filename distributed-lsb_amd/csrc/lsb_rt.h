@@ -284,8 +284,11 @@ lsb_ctx* new_ctx(int64_t n_total, int num_ranks, int radix_bits);
 // ---- collectives (lsb_context.cpp) ------------------------------------------
 int ops_fail(const char* what);
 int coll_allgather_u64(lsb_ctx* c, Rank& r, const uint64_t* send, uint64_t* recv, size_t count);
+// RCCL calls carry at most this many u64 (1 GiB) per peer (coll_alltoallv_u64).
+constexpr size_t kMaxCallU64 = (size_t)1 << 27;
 int coll_alltoallv_u64(lsb_ctx* c, Rank& r, const uint64_t* send, const size_t* sc,
-                       const size_t* sd, uint64_t* recv, const size_t* rc, const size_t* rd);
+                       const size_t* sd, uint64_t* recv, const size_t* rc, const size_t* rd,
+                       size_t bound);
 int gather_boundaries(lsb_ctx* c, std::vector<uint64_t>& bnd);
 int allreduce_min_i64(lsb_ctx* c, int64_t* v);
 int gather_span(lsb_ctx* c, uint64_t* kor, uint64_t* knor);
@@ -353,6 +356,12 @@ inline int64_t slice_part(int64_t n, int j, int slices) {
 // every record: its last slice's merge (ceil(log2 P) levels) is the tail
 // after the wire goes quiet.
 inline int slices_of(const lsb_ctx* c) { return c->slices > 0 ? c->slices : (c->bits == 64 ? 8 : 5); }
+
+// Records of slice j of any peer segment of a rank block of `per` records, at
+// most (slice_part is monotone in the segment length, which is <= per).
+inline int64_t slice_bound(int64_t per, int j, int slices) {
+  return slice_part(per, j + 1, slices) - slice_part(per, j, slices) + 1;
+}
 int ensure_recv(lsb_ctx* c, Rank& r);
 int join_place(Rank& r);
 int join_place_timed(lsb_ctx* c, Rank& r);

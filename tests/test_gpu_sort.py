@@ -384,6 +384,29 @@ def test_rccl_world_of_one(lsb_built, oracle_mod, digests, p2p):
         w.close()
 
 
+@pytest.mark.parametrize("lg,bits,slices", [(27, 16, 0), (28, 16, 0), (28, 8, 1), (28, 64, 1)])
+def test_world_of_one_large_calls(lsb_built, lg, bits, slices):
+    """The bench's x16 extra at smaller sizes: every record through
+    ncclAllToAllv of a world-of-one RCCL communicator, with slices whose
+    per-peer range reaches 1 GiB (2^27 records, first halving slice), 2 GiB
+    (2^28) and, in one slice, 4 GiB.  RCCL moved ranges of 2 GiB or more
+    wrongly (verify false at 2^28 in round 5); the runtime now cuts such a
+    call into calls of at most 1 GiB per peer (coll_alltoallv_u64)."""
+    n = 1 << lg
+    w = lsb_built.World.rank(n, 1, 0, 0, lsb_built.get_unique_id(), radix_bits=bits)
+    try:
+        w.set_option(lsb_built.OPT_FORCE_EXCHANGE, 1)
+        w.set_option(lsb_built.OPT_EXCHANGE_SELF, 1)
+        if slices:
+            w.set_option(lsb_built.OPT_EXCHANGE_SLICES, slices)
+        w.generate()
+        w.my_sort()
+        assert w.verify() == (True, -1)
+        assert w.exchange_stats()["sent_bytes"][0] > 0
+    finally:
+        w.close()
+
+
 @pytest.mark.parametrize("bits,slices", [(16, 4), (8, 3), (64, 5)])
 def test_exchange_stats_world_of_one(lsb_built, oracle_mod, digests, bits, slices):
     """lsb_get_exchange_stats through real RCCL: a world of one with the

@@ -25,10 +25,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 TOOL = os.path.join(ROOT, "tools", "rccl_two_ranks.py")
 
 
-def _run(bits, n, world, exchange="alltoallv", slices=0, dist="uniform", dump=""):
+def _run(bits, n, world, exchange="alltoallv", slices=0, dist="uniform", dump="", env=None):
     p = subprocess.run([sys.executable, "-u", TOOL, str(bits), str(n), str(world), exchange, str(slices),
                         dist, dump],
-                       capture_output=True, text=True, timeout=240, cwd=ROOT)
+                       capture_output=True, text=True, timeout=240, cwd=ROOT,
+                       env=dict(os.environ, **(env or {})))
     lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
     assert lines, f"rc={p.returncode}\n{p.stdout[-2000:]}\n{p.stderr[-2000:]}"
     return p.returncode, json.loads(lines[-1])
@@ -74,3 +75,19 @@ def test_real_rccl_ranks_zipf(lsb_built, oracle_mod, tmp_path, bits, n, world, e
     out = np.concatenate([np.load(tmp_path / f"out_{q}.npy") for q in range(world)])
     assert inp.size == n and np.unique(inp["key"]).size < n // 2  # heavy duplicates
     assert np.array_equal(out, oracle_mod.stable_sort(inp))
+
+
+@pytest.mark.parametrize("bits,n,world,exchange", [
+    (16, 1_000_003, 4, "alltoallv"),
+    (64, 1_000_000, 2, "p2p"),
+])
+def test_real_rccl_ranks_vmm_pieces(lsb_built, bits, n, world, exchange):
+    """Record buffers built from 2 MiB VMM pieces (LSB_VMM_CHUNK_MIB=2; at
+    2^30 records per rank they are 1 GiB pieces) as RCCL's send and receive
+    buffers between real ranks: the golden digest, every rank verified."""
+    rc, r = _run(bits, n, world, exchange, env={"LSB_VMM_CHUNK_MIB": "2"})
+    assert r["status"] == "ok", r
+    assert r["golden_match"] is True, r
+    assert all(r["verify"]) and all(r["check_sorted"]), r
+    assert all(b > 0 for b in r["rccl_bytes"]), r
+    assert rc == 0
