@@ -91,3 +91,15 @@ def test_real_rccl_ranks_vmm_pieces(lsb_built, bits, n, world, exchange):
     assert all(r["verify"]) and all(r["check_sorted"]), r
     assert all(b > 0 for b in r["rccl_bytes"]), r
     assert rc == 0
+
+
+def test_real_rccl_ranks_two_gib_segments(lsb_built):
+    """Two real ranks of 2^28 records each, one slice per exchange: each
+    rank's segment to its peer is ~2 GiB per call, which RCCL moves wrongly in
+    one piece; the runtime cuts it into calls of at most 1 GiB per peer
+    (coll_alltoallv_u64).  Verified on device on both ranks."""
+    rc, r = _run(16, 1 << 29, 2, "alltoallv", 1)
+    assert r["status"] == "ok", r
+    assert all(r["verify"]) and all(r["check_sorted"]), r
+    assert all(b >= (1 << 31) for b in r["rccl_bytes"]), r  # >= 2 GiB handed to RCCL per rank
+    assert rc == 0

@@ -60,12 +60,13 @@ def worker(rank, world, n, bits, exchange, slices, dist, dump, q_uid, q_out):
         ok, bad = w.verify()
         sorted_ = w.check_sorted()
         _, xbytes, xmax = w.exchange_bytes()
-        out = w.copy_out(rank)
+        # large blocks are checked on device only (lsb_verify), not digested
+        out = w.copy_out(rank) if n <= (1 << 26) or dump else None
         if dump:
             import numpy as np
             np.save(os.path.join(dump, f"out_{rank}.npy"), out)
         w.close()
-        q_out.put((rank, "ok", ok, bad, sorted_, out.tobytes(), xbytes, xmax))
+        q_out.put((rank, "ok", ok, bad, sorted_, out.tobytes() if out is not None else b"", xbytes, xmax))
     except Exception as e:  # report, never hang the parent
         q_out.put((rank, "error", repr(e), None, None, b"", 0, 0))
 
@@ -94,7 +95,7 @@ def main():
     if errors:
         print(json.dumps({"status": "error", "errors": errors}))
         sys.exit(1)
-    digest = hashlib.sha256(b"".join(res[r][5] for r in range(world))).hexdigest()
+    digest = hashlib.sha256(b"".join(res[r][5] for r in range(world))).hexdigest() if n <= (1 << 26) else None
     golden = json.load(open(os.path.join(ROOT, "tests", "golden", "digests.json")))
     want = None if dist != "uniform" else next(
         (g["output"] for g in golden["rows"] if g["n"] == n and g["P"] == world), None)
