@@ -358,9 +358,10 @@ inline int64_t slice_part(int64_t n, int j, int slices) {
 inline int slices_of(const lsb_ctx* c) { return c->slices > 0 ? c->slices : (c->bits == 64 ? 8 : 5); }
 
 // Records of slice j of any peer segment of a rank block of `per` records, at
-// most (slice_part is monotone in the segment length, which is <= per).
+// most: a slice of a segment of n records holds ceil(floor(n / 2^j) / 2) (the
+// last: floor(n / 2^(S-1))), non-decreasing in n, and n <= per.
 inline int64_t slice_bound(int64_t per, int j, int slices) {
-  return slice_part(per, j + 1, slices) - slice_part(per, j, slices) + 1;
+  return slice_part(per, j + 1, slices) - slice_part(per, j, slices);
 }
 int ensure_recv(lsb_ctx* c, Rank& r);
 int join_place(Rank& r);

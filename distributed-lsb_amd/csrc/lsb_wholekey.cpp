@@ -300,7 +300,7 @@ int exchange_merge(lsb_ctx* c) {
         // an owner's slice holds at most ceil(per / S) records, from all sources together
         LSB_TRY(coll_alltoallv_u64(c, r, reinterpret_cast<const uint64_t*>(r.A), sc.data(), sd.data(),
                                    reinterpret_cast<uint64_t*>(r.R), rc.data(), rdp.data(),
-                                   (size_t)(c->per / g.S + 2) * 2));
+                                   (size_t)div_ceil(c->per, g.S) * 2));
       }
       LSB_TRY(merge_slice_async(c, r, g, j, final_b ? r.B : r.R));
     }
