@@ -152,7 +152,13 @@ int64_t lsb_here(int64_t n_total, int num_ranks, int rank);      /* clamp(n - r*
  * radix_bits = 64 makes the whole key one digit: each rank sorts its block
  * (all 8 local passes), then ONE all-to-all moves every record to its owner,
  * which merges the P sorted runs in rank order (lsb_plan_merge).  Same
- * output again; one exchange per sort instead of 64 / radix_bits. */
+ * output again; one exchange per sort instead of 64 / radix_bits.
+ * Device memory per rank: lsb_rank_footprint (A and B here; R, the receive
+ * buffer, at the first exchange or hybrid sort; record buffers of >= 1 GiB
+ * are whole 1 GiB VMM pieces).  With LSB_PLACEMENT_CANDIDATES = K > 2 a
+ * rank alone on its device also holds K - 2 more record buffers while its
+ * placement probe runs (lsb_get_placement), as many as fit in 90 % of the
+ * free memory at that moment. */
 int  lsb_create(lsb_ctx_t** ctx, int64_t n_total, int num_ranks,
                 const int* dev_ids, int radix_bits);
 /* HIP devices this process can see (hipGetDeviceCount; 0 when there is
