@@ -44,9 +44,13 @@ int lsb_create(lsb_ctx_t** out, int64_t n_total, int num_ranks, const int* dev_i
   c->mode = Mode::kLoopback;
   c->first_rank = 0;
   c->ranks.resize(num_ranks);
-  for (int r = 0; r < num_ranks; ++r)
+  for (int r = 0; r < num_ranks; ++r) {
+    const int d = dev_ids ? dev_ids[r] : 0;
     for (int q = 0; q < r; ++q)
-      if ((dev_ids ? dev_ids[r] : 0) == (dev_ids ? dev_ids[q] : 0)) c->shared_device = true;
+      if (d == (dev_ids ? dev_ids[q] : 0)) c->shared_device = true;
+    if (std::find(c->access_devs.begin(), c->access_devs.end(), d) == c->access_devs.end())
+      c->access_devs.push_back(d);
+  }
   for (int r = 0; r < num_ranks; ++r) {
     int rc = init_rank(c, c->ranks[r], r, dev_ids ? dev_ids[r] : 0);
     if (rc != LSB_OK) {

@@ -89,10 +89,11 @@ int max_chunks_for_device(int dev) {
 // some (the driver's choice of physical pages), while between buffers built
 // from 1 GiB pieces it runs at 5.7-6.8 ms (tools/kbench/vmmbw.hip,
 // profiles/r05/vmm_*; DESIGN.md §4 "Spread").  LSB_RECORD_ALLOC=malloc keeps
-// hipMalloc.  Pieces are readable and writable by every device that can
-// access this one (hipMemSetAccess), as hipMalloc memory is once peer access
-// is enabled; IPC handles cannot name them, so the peer-store exchange moves
-// the records into hipMalloc buffers at its setup (peer_setup).
+// hipMalloc.  Pieces are readable and writable by the owner and by the other
+// devices of a loopback context's ranks (hipMemSetAccess), as hipMalloc
+// memory is once peer access is enabled; IPC handles cannot name them, so the
+// peer-store exchange between processes moves the records into hipMalloc
+// buffers at its setup (peer_setup).
 namespace {
 
 struct VmmBuffer {
@@ -137,7 +138,7 @@ bool rec_is_vmm(const void* p) {
   return false;
 }
 
-int rec_alloc(Elem** out, size_t count) {
+int rec_alloc(const lsb_ctx* c, Elem** out, size_t count) {
   *out = nullptr;
   const size_t piece = vmm_piece_bytes();
   const size_t want = std::max<size_t>(count, 1) * sizeof(Elem);
@@ -171,12 +172,13 @@ int rec_alloc(Elem** out, size_t count) {
     }
   }
   if (e == hipSuccess) {
-    // this device, and every device that can reach it (as peer access does for hipMalloc)
-    int ndev = 0;
-    (void)hipGetDeviceCount(&ndev);
+    // This device, and the other devices of the context's ranks (loopback
+    // contexts over several GPUs copy between them; a one-rank-per-process
+    // context maps its buffers for its own device only, so no process sets up
+    // mappings on the other GPUs of a node).
     std::vector<hipMemAccessDesc> acc;
-    for (int k = -1; k < ndev; ++k) {  // the owner first
-      const int d = k < 0 ? dev : k;
+    for (int k = -1; k < (int)c->access_devs.size(); ++k) {  // the owner first
+      const int d = k < 0 ? dev : c->access_devs[k];
       int can = k < 0;
       if (k >= 0 && (d == dev || hipDeviceCanAccessPeer(&can, d, dev) != hipSuccess)) can = 0;
       if (!can) continue;
@@ -269,11 +271,11 @@ struct Prober {
 };
 
 // Up to K buffers of per records (at least `need`).
-int alloc_candidates(size_t per, int K, size_t need, std::vector<Elem*>& cand) {
+int alloc_candidates(const lsb_ctx* c, size_t per, int K, size_t need, std::vector<Elem*>& cand) {
   cand.clear();
   for (int k = 0; k < K; ++k) {
     Elem* p = nullptr;
-    if (rec_alloc(&p, per) != LSB_OK) break;  // fewer candidates than hoped
+    if (rec_alloc(c, &p, per) != LSB_OK) break;  // fewer candidates than hoped
     cand.push_back(p);
   }
   (void)hipGetLastError();
@@ -334,11 +336,11 @@ int alloc_records(lsb_ctx* c, Rank& r) {
   int K = c->shared_device ? 0 : placement_candidates((double)per * sizeof(Elem), 8);
   r.placement_k = 0;
   if (K <= 2 || r.here < (int64_t)lsb::kTile * lsb::kOnesweepSubs || r.here > lsb::kOnesweepMaxElems) {
-    LSB_TRY(rec_alloc(&r.A, per));
-    return rec_alloc(&r.B, per);
+    LSB_TRY(rec_alloc(c, &r.A, per));
+    return rec_alloc(c, &r.B, per);
   }
   std::vector<Elem*> cand;
-  LSB_TRY(alloc_candidates(per, K, 2, cand));
+  LSB_TRY(alloc_candidates(c, per, K, 2, cand));
   K = (int)cand.size();
   auto give_up = [&](int rc) {
     for (Elem* p : cand) rec_free(p);
@@ -408,9 +410,9 @@ int alloc_third(lsb_ctx* c, Rank& r) {
   const size_t per = (size_t)c->per;
   int K = r.placement_k > 0 ? placement_candidates((double)per * sizeof(Elem), 3) : 1;  // probed A and B only
   if (K <= 2) K = 1;
-  if (K == 1 || !r.os_status) return rec_alloc(&r.R, per);
+  if (K == 1 || !r.os_status) return rec_alloc(c, &r.R, per);
   std::vector<Elem*> cand;
-  LSB_TRY(alloc_candidates(per, K, 1, cand));
+  LSB_TRY(alloc_candidates(c, per, K, 1, cand));
   K = (int)cand.size();
   uint32_t* hist = nullptr;
   int rc = K > 1 ? dev_alloc(&hist, (size_t)lsb::kOnesweepSubs * lsb::kBuckets) : LSB_OK;

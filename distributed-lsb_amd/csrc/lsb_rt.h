@@ -139,6 +139,7 @@ struct lsb_ctx {
   lsb_comm_ops_t ops = {};  // Mode::kOps
   bool timing = false;
   bool shared_device = false;  // two local ranks on one device (no placement probe)
+  std::vector<int> access_devs;  // loopback: every device of the ranks (VMM record buffers map on all)
   bool force_exchange = false;
   bool skip_constant = true;  // lsb_sort skips digits on which all keys agree
   int slices = 0;             // exchange slices (placement overlaps the next slice); 0 = default
@@ -268,7 +269,7 @@ int host_alloc(T** p, size_t count) {
 // ---- context and rank buffers (lsb_context.cpp) -------------------------------
 // Record buffers (A, B, R, candidates): VMM-backed in 1 GiB pieces when at
 // least one piece long, else hipMalloc; rec_free frees either kind.
-int rec_alloc(Elem** p, size_t count);
+int rec_alloc(const lsb_ctx* c, Elem** p, size_t count);
 size_t rec_bytes(size_t count);  // device bytes rec_alloc takes for count records
 void rec_free(void* p);
 bool rec_is_vmm(const void* p);
