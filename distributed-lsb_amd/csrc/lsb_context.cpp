@@ -138,11 +138,23 @@ bool rec_is_vmm(const void* p) {
   return false;
 }
 
-int rec_alloc(const lsb_ctx* c, Elem** out, size_t count) {
-  *out = nullptr;
+// k record buffers of `count` records each.  VMM pieces are created in the
+// order LSB_VMM_ORDER names: buffer by buffer (default), or "interleave"
+// (piece j of every buffer before piece j + 1 of any).
+int rec_alloc_group(const lsb_ctx* c, Elem** const* outs, int k, size_t count) {
+  for (int i = 0; i < k; ++i) *outs[i] = nullptr;
   const size_t piece = vmm_piece_bytes();
   const size_t want = std::max<size_t>(count, 1) * sizeof(Elem);
-  if (piece == 0 || want < piece) return dev_alloc(out, count);
+  if (piece == 0 || want < piece) {
+    for (int i = 0; i < k; ++i) {
+      const int rc = dev_alloc(outs[i], count);
+      if (rc != LSB_OK) {
+        for (int q = 0; q < i; ++q) (void)hipFree(*outs[q]);
+        return rc;
+      }
+    }
+    return LSB_OK;
+  }
   int dev = 0;
   HIP_TRY(hipGetDevice(&dev));
   hipMemAllocationProp prop = {};
@@ -152,55 +164,67 @@ int rec_alloc(const lsb_ctx* c, Elem** out, size_t count) {
   size_t gran = 0;
   HIP_TRY(hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum));
   if (gran == 0 || piece % gran) return fail(LSB_ERR_INVALID, "rec_alloc", "LSB_VMM_CHUNK_MIB is not a multiple of the granularity");
-  VmmBuffer b;
-  b.bytes = (want + piece - 1) / piece * piece;
-  hipError_t e = hipMemAddressReserve(&b.base, b.bytes, piece, nullptr, 0);
-  if (e != hipSuccess) {
-    b.base = nullptr;
-    return fail(LSB_ERR_NOMEM, "hipMemAddressReserve", hipGetErrorString(e));
+  const char* order = getenv("LSB_VMM_ORDER");
+  const bool interleave = order && strcmp(order, "interleave") == 0;
+  std::vector<VmmBuffer> b((size_t)k);
+  const size_t bytes = (want + piece - 1) / piece * piece, np = bytes / piece;
+  hipError_t e = hipSuccess;
+  for (int i = 0; i < k && e == hipSuccess; ++i) {
+    b[i].bytes = bytes;
+    b[i].piece = piece;
+    e = hipMemAddressReserve(&b[i].base, bytes, piece, nullptr, 0);
+    if (e != hipSuccess) b[i].base = nullptr;
   }
-  for (size_t off = 0; off < b.bytes; off += piece) {
+  // piece j of buffer i, in creation order (pieces of a buffer map in order)
+  for (size_t t = 0; t < np * (size_t)k && e == hipSuccess; ++t) {
+    const int i = interleave ? (int)(t % (size_t)k) : (int)(t / np);
+    const size_t j = b[i].pieces.size();
     hipMemGenericAllocationHandle_t h;
     e = hipMemCreate(&h, piece, &prop, 0);
     if (e != hipSuccess) break;
-    b.pieces.push_back(h);
-    e = hipMemMap(static_cast<char*>(b.base) + off, piece, 0, h, 0);
+    e = hipMemMap(static_cast<char*>(b[i].base) + j * piece, piece, 0, h, 0);
     if (e != hipSuccess) {
       (void)hipMemRelease(h);
-      b.pieces.pop_back();
       break;
     }
+    b[i].pieces.push_back(h);
   }
-  if (e == hipSuccess) {
-    // This device, and the other devices of the context's ranks (loopback
-    // contexts over several GPUs copy between them; a one-rank-per-process
-    // context maps its buffers for its own device only, so no process sets up
-    // mappings on the other GPUs of a node).
-    std::vector<hipMemAccessDesc> acc;
-    for (int k = -1; k < (int)c->access_devs.size(); ++k) {  // the owner first
-      const int d = k < 0 ? dev : c->access_devs[k];
-      int can = k < 0;
-      if (k >= 0 && (d == dev || hipDeviceCanAccessPeer(&can, d, dev) != hipSuccess)) can = 0;
-      if (!can) continue;
-      hipMemAccessDesc a = {};
-      a.location.type = hipMemLocationTypeDevice;
-      a.location.id = d;
-      a.flags = hipMemAccessFlagsProtReadWrite;
-      acc.push_back(a);
-    }
-    e = hipMemSetAccess(b.base, b.bytes, acc.data(), acc.size());
-    if (e != hipSuccess && acc.size() > 1) e = hipMemSetAccess(b.base, b.bytes, acc.data(), 1);  // owner only
+  // This device, and the other devices of the context's ranks (loopback
+  // contexts over several GPUs copy between them; a one-rank-per-process
+  // context maps its buffers for its own device only, so no process sets up
+  // mappings on the other GPUs of a node).
+  std::vector<hipMemAccessDesc> acc;
+  for (int q = -1; q < (int)c->access_devs.size(); ++q) {  // the owner first
+    const int d = q < 0 ? dev : c->access_devs[q];
+    int can = q < 0;
+    if (q >= 0 && (d == dev || hipDeviceCanAccessPeer(&can, d, dev) != hipSuccess)) can = 0;
+    if (!can) continue;
+    hipMemAccessDesc a = {};
+    a.location.type = hipMemLocationTypeDevice;
+    a.location.id = d;
+    a.flags = hipMemAccessFlagsProtReadWrite;
+    acc.push_back(a);
+  }
+  for (int i = 0; i < k && e == hipSuccess; ++i) {
+    e = hipMemSetAccess(b[i].base, bytes, acc.data(), acc.size());
+    if (e != hipSuccess && acc.size() > 1) e = hipMemSetAccess(b[i].base, bytes, acc.data(), 1);  // owner only
   }
   if (e != hipSuccess) {
     const std::string why = hipGetErrorString(e);
-    vmm_release(b, piece);
+    for (VmmBuffer& x : b) vmm_release(x, piece);
     return fail(LSB_ERR_NOMEM, "rec_alloc (hipMemCreate / hipMemMap / hipMemSetAccess)", why.c_str());
   }
-  b.piece = piece;
-  *out = static_cast<Elem*>(b.base);
   std::lock_guard<std::mutex> lock(g_vmm_mu);
-  g_vmm.push_back(std::move(b));
+  for (int i = 0; i < k; ++i) {
+    *outs[i] = static_cast<Elem*>(b[i].base);
+    g_vmm.push_back(std::move(b[i]));
+  }
   return LSB_OK;
+}
+
+int rec_alloc(const lsb_ctx* c, Elem** out, size_t count) {
+  Elem** const outs[1] = {out};
+  return rec_alloc_group(c, outs, 1, count);
 }
 
 void rec_free(void* p) {
@@ -336,8 +360,10 @@ int alloc_records(lsb_ctx* c, Rank& r) {
   int K = c->shared_device ? 0 : placement_candidates((double)per * sizeof(Elem), 8);
   r.placement_k = 0;
   if (K <= 2 || r.here < (int64_t)lsb::kTile * lsb::kOnesweepSubs || r.here > lsb::kOnesweepMaxElems) {
-    LSB_TRY(rec_alloc(c, &r.A, per));
-    return rec_alloc(c, &r.B, per);
+    // LSB_ALLOC_R_EARLY=1 (experiment): R with A and B, at creation
+    const char* early = getenv("LSB_ALLOC_R_EARLY");
+    Elem** const outs[3] = {&r.A, &r.B, &r.R};
+    return rec_alloc_group(c, outs, early && atoi(early) ? 3 : 2, per);
   }
   std::vector<Elem*> cand;
   LSB_TRY(alloc_candidates(c, per, K, 2, cand));

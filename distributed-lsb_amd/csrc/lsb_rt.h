@@ -270,6 +270,7 @@ int host_alloc(T** p, size_t count) {
 // Record buffers (A, B, R, candidates): VMM-backed in 1 GiB pieces when at
 // least one piece long, else hipMalloc; rec_free frees either kind.
 int rec_alloc(const lsb_ctx* c, Elem** p, size_t count);
+int rec_alloc_group(const lsb_ctx* c, Elem** const* outs, int k, size_t count);
 size_t rec_bytes(size_t count);  // device bytes rec_alloc takes for count records
 void rec_free(void* p);
 bool rec_is_vmm(const void* p);

@@ -39,6 +39,9 @@ for c in range(ctxs):
         os.environ["LSB_PLACEMENT_PICK"] = picks[c % len(picks)]
     w = lsbsort.World(n, ranks=1, radix_bits=8)
     worlds.append(w)
+    # LSB_PROBE_HYBRID=1: the hybrid local sort (passes A -> B -> R ...: the
+    # third record buffer's pairs; R is allocated at its first sort)
+    w.set_option(lsbsort.OPT_HYBRID, int(os.environ.get("LSB_PROBE_HYBRID", "0")))
     w.generate()
     w.my_sort()  # warm-up (allocates the look-back rows)
     w.sync()

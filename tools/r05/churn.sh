@@ -4,7 +4,7 @@
 # tools/alloc_probe.py before and after a part of the suite, GPU temperature
 # and memory use beside them.  Output: gpurun_out/r05_churn/.
 set -u
-O=gpurun_out/r05_churn
+O=gpurun_out/${TAG:-r05_churn}
 mkdir -p $O
 state() { timeout -k 5 30 rocm-smi --showtemp --showmemuse > $O/smi_$1.txt 2>&1; grep -iE "junction|memory.*temp|vram%|use" $O/smi_$1.txt | head -6; }
 ap() {
@@ -15,7 +15,7 @@ ap() {
 state before
 ap pre_vmm1
 ap pre_vmm2
-timeout -k 10 400 python -u -m pytest tests/test_gpu_sort.py tests/test_onesweep_gpu.py -m gpu -x -q --timeout 200 \
+timeout -k 10 800 python -u -m pytest ${CHURN_TESTS:-tests/test_gpu_sort.py tests/test_onesweep_gpu.py} -m gpu -x -q --timeout 300 \
   --timeout-method thread > $O/tests.log 2>&1 || { tail -20 $O/tests.log; exit 1; }
 tail -1 $O/tests.log
 state after
