@@ -410,6 +410,18 @@ int exchange_rccl(lsb_ctx* c, int digit) {
   plan_fetch(c, r);
   LSB_TRY(place_self(c, r, shift));
   const int me = r.rank;
+  // Calls of more than 1 GiB per peer are cut (coll_alltoallv_u64), alike on
+  // every rank: by the largest peer segment of this exchange on any rank, one
+  // all-reduce of one word, asked only when a block could exceed it at all.
+  int64_t seg = c->per;
+  if (c->mode == Mode::kRccl && (size_t)slice_bound(c->per, 0, slices_of(c)) * 2 > kMaxCallU64) {
+    int64_t m = 0;
+    for (int q = 0; q < P; ++q)
+      if (q != me || c->self_coll) m = std::max(m, std::max(r.send_counts[q], r.recv_counts[q]));
+    int64_t neg = -m;
+    LSB_TRY(allreduce_min_i64(c, &neg));
+    seg = -neg;
+  }
   // ncclAllToAllv per slice (the reference's MPI_Alltoallv,
   // mpi/mpi_lsbsort.cpp:316-324), in uint64 units; the self entry is 0
   // because the self segment was placed straight out of A (unless
@@ -431,7 +443,7 @@ int exchange_rccl(lsb_ctx* c, int digit) {
       }
       LSB_TRY(coll_alltoallv_u64(c, r, reinterpret_cast<const uint64_t*>(r.A), sc.data(),
                                  sd.data(), reinterpret_cast<uint64_t*>(r.R), rc.data(),
-                                 rdp.data(), (size_t)slice_bound(c->per, j, slices_of(c)) * 2));
+                                 rdp.data(), (size_t)slice_bound(seg, j, slices_of(c)) * 2));
     }
     LSB_TRY(place_slice(c, r, shift, j));
   }

@@ -269,6 +269,14 @@ int exchange_merge(lsb_ctx* c) {
   const bool final_b = (merge_levels((size_t)P) - 1) % 2 == 0;
   std::vector<SliceRun> sr;
   int64_t lo = 0, hi = 0;
+  // The longest range any source sends to any (owner, slice): every rank holds
+  // every source's cuts, so all cut their RCCL calls alike (coll_alltoallv_u64).
+  int64_t run_max = 0;
+  {
+    const std::vector<int64_t>& mc = c->ranks[0].mcut;
+    for (size_t s = 0; s < (size_t)P; ++s)
+      for (size_t k = 0; k + 1 < K1; ++k) run_max = std::max(run_max, mc[s * K1 + k + 1] - mc[s * K1 + k]);
+  }
   for (int j = 0; j < g.S; ++j) {
     if (c->mode == Mode::kLoopback) {
       for (Rank& q : c->ranks) {
@@ -297,10 +305,9 @@ int exchange_merge(lsb_ctx* c) {
       }
       {
         Timer t(c, &r, LSB_K_WIRE);
-        // an owner's slice holds at most ceil(per / S) records, from all sources together
         LSB_TRY(coll_alltoallv_u64(c, r, reinterpret_cast<const uint64_t*>(r.A), sc.data(), sd.data(),
                                    reinterpret_cast<uint64_t*>(r.R), rc.data(), rdp.data(),
-                                   (size_t)div_ceil(c->per, g.S) * 2));
+                                   (size_t)run_max * 2));
       }
       LSB_TRY(merge_slice_async(c, r, g, j, final_b ? r.B : r.R));
     }
