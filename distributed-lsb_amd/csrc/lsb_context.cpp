@@ -1,11 +1,10 @@
 // Context and rank state of the runtime behind include/lsb.h: errors, HIP-event
-// timing of launches (filed per local pass, lsb_get_pass_stats), device
-// buffers of a rank (DistributedArray::create, mpi/mpi_lsbsort.cpp:137-161),
-// and the collectives of a one-rank-per-process context (RCCL, or the
-// caller's host callbacks) that the pass driver and both exchange forms use.
+// timing of launches (filed per local pass, lsb_get_pass_stats), a rank's
+// buffers (DistributedArray::create, mpi/mpi_lsbsort.cpp:137-161; the record
+// buffers themselves come from lsb_alloc.cpp), and the collectives of a
+// one-rank-per-process context (RCCL, or the caller's host callbacks) that
+// the pass driver and both exchange forms use.
 #include "lsb_rt.h"
-
-#include <mutex>
 
 namespace lsb_rt {
 
@@ -78,393 +77,6 @@ int max_chunks_for_device(int dev) {
   if (hipGetDeviceProperties(&prop, dev) != hipSuccess || prop.multiProcessorCount <= 0) return 512;
   // Two scatter workgroups fit one CU (72 KiB LDS each): one chunk per slot.
   return std::min(lsb::kMaxChunks, 2 * prop.multiProcessorCount);
-}
-
-// ---- record buffers: physical memory in 1 GiB pieces ---------------------------
-// A record buffer of at least one piece (LSB_VMM_CHUNK_MIB, default 1024) is
-// not a hipMalloc: its address range is reserved once and backed by
-// separately created 1 GiB physical allocations (hipMemCreate + hipMemMap,
-// HIP's virtual memory management).  The same LSD write pattern between two
-// hipMalloc'd 16 GiB buffers runs at 6.85 ms for most pairs and 7.2 ms for
-// some (the driver's choice of physical pages), while between buffers built
-// from 1 GiB pieces it runs at 5.7-6.8 ms (tools/kbench/vmmbw.hip,
-// profiles/r05/vmm_*; DESIGN.md §4 "Spread").  LSB_RECORD_ALLOC=malloc keeps
-// hipMalloc.  Pieces are readable and writable by the owner and by the other
-// devices of a loopback context's ranks (hipMemSetAccess), as hipMalloc
-// memory is once peer access is enabled; IPC handles cannot name them, so the
-// peer-store exchange between processes moves the records into hipMalloc
-// buffers at its setup (peer_setup).
-namespace {
-
-struct VmmBuffer {
-  void* base = nullptr;
-  size_t bytes = 0;
-  size_t piece = 0;
-  std::vector<hipMemGenericAllocationHandle_t> pieces;
-};
-std::mutex g_vmm_mu;
-std::vector<VmmBuffer> g_vmm;  // live VMM record buffers of this process
-
-size_t vmm_piece_bytes() {
-  const char* mode = getenv("LSB_RECORD_ALLOC");
-  if (mode && strcmp(mode, "malloc") == 0) return 0;
-  size_t mib = 1024;
-  if (const char* e = getenv("LSB_VMM_CHUNK_MIB")) mib = (size_t)std::max(0ll, atoll(e));
-  return mib << 20;
-}
-
-// Unmaps and releases the first pieces.size() pieces of `piece` bytes (mapped
-// in order from the base) and frees the address range.
-void vmm_release(VmmBuffer& b, size_t piece) {
-  for (size_t k = 0; k < b.pieces.size(); ++k) (void)hipMemUnmap(static_cast<char*>(b.base) + k * piece, piece);
-  for (auto h : b.pieces) (void)hipMemRelease(h);
-  if (b.base) (void)hipMemAddressFree(b.base, b.bytes);
-  (void)hipGetLastError();
-  b = VmmBuffer();
-}
-
-}  // namespace
-
-size_t rec_bytes(size_t count) {
-  const size_t piece = vmm_piece_bytes();
-  const size_t want = std::max<size_t>(count, 1) * sizeof(Elem);
-  return piece == 0 || want < piece ? want : (want + piece - 1) / piece * piece;
-}
-
-bool rec_is_vmm(const void* p) {
-  std::lock_guard<std::mutex> lock(g_vmm_mu);
-  for (const VmmBuffer& b : g_vmm)
-    if (b.base == p) return true;
-  return false;
-}
-
-// k record buffers of `count` records each.  VMM pieces are created in the
-// order LSB_VMM_ORDER names: buffer by buffer (default), or "interleave"
-// (piece j of every buffer before piece j + 1 of any).
-int rec_alloc_group(const lsb_ctx* c, Elem** const* outs, int k, size_t count) {
-  for (int i = 0; i < k; ++i) *outs[i] = nullptr;
-  const size_t piece = vmm_piece_bytes();
-  const size_t want = std::max<size_t>(count, 1) * sizeof(Elem);
-  if (piece == 0 || want < piece) {
-    for (int i = 0; i < k; ++i) {
-      const int rc = dev_alloc(outs[i], count);
-      if (rc != LSB_OK) {
-        for (int q = 0; q < i; ++q) (void)hipFree(*outs[q]);
-        return rc;
-      }
-    }
-    return LSB_OK;
-  }
-  int dev = 0;
-  HIP_TRY(hipGetDevice(&dev));
-  hipMemAllocationProp prop = {};
-  prop.type = hipMemAllocationTypePinned;
-  prop.location.type = hipMemLocationTypeDevice;
-  prop.location.id = dev;
-  size_t gran = 0;
-  HIP_TRY(hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum));
-  if (gran == 0 || piece % gran) return fail(LSB_ERR_INVALID, "rec_alloc", "LSB_VMM_CHUNK_MIB is not a multiple of the granularity");
-  const char* order = getenv("LSB_VMM_ORDER");
-  const bool interleave = order && strcmp(order, "interleave") == 0;
-  std::vector<VmmBuffer> b((size_t)k);
-  const size_t bytes = (want + piece - 1) / piece * piece, np = bytes / piece;
-  hipError_t e = hipSuccess;
-  for (int i = 0; i < k && e == hipSuccess; ++i) {
-    b[i].bytes = bytes;
-    b[i].piece = piece;
-    e = hipMemAddressReserve(&b[i].base, bytes, piece, nullptr, 0);
-    if (e != hipSuccess) b[i].base = nullptr;
-  }
-  // piece j of buffer i, in creation order (pieces of a buffer map in order)
-  for (size_t t = 0; t < np * (size_t)k && e == hipSuccess; ++t) {
-    const int i = interleave ? (int)(t % (size_t)k) : (int)(t / np);
-    const size_t j = b[i].pieces.size();
-    hipMemGenericAllocationHandle_t h;
-    e = hipMemCreate(&h, piece, &prop, 0);
-    if (e != hipSuccess) break;
-    e = hipMemMap(static_cast<char*>(b[i].base) + j * piece, piece, 0, h, 0);
-    if (e != hipSuccess) {
-      (void)hipMemRelease(h);
-      break;
-    }
-    b[i].pieces.push_back(h);
-  }
-  // This device, and the other devices of the context's ranks (loopback
-  // contexts over several GPUs copy between them; a one-rank-per-process
-  // context maps its buffers for its own device only, so no process sets up
-  // mappings on the other GPUs of a node).
-  std::vector<hipMemAccessDesc> acc;
-  for (int q = -1; q < (int)c->access_devs.size(); ++q) {  // the owner first
-    const int d = q < 0 ? dev : c->access_devs[q];
-    int can = q < 0;
-    if (q >= 0 && (d == dev || hipDeviceCanAccessPeer(&can, d, dev) != hipSuccess)) can = 0;
-    if (!can) continue;
-    hipMemAccessDesc a = {};
-    a.location.type = hipMemLocationTypeDevice;
-    a.location.id = d;
-    a.flags = hipMemAccessFlagsProtReadWrite;
-    acc.push_back(a);
-  }
-  for (int i = 0; i < k && e == hipSuccess; ++i) {
-    e = hipMemSetAccess(b[i].base, bytes, acc.data(), acc.size());
-    if (e != hipSuccess && acc.size() > 1) e = hipMemSetAccess(b[i].base, bytes, acc.data(), 1);  // owner only
-  }
-  if (e != hipSuccess) {
-    const std::string why = hipGetErrorString(e);
-    for (VmmBuffer& x : b) vmm_release(x, piece);
-    return fail(LSB_ERR_NOMEM, "rec_alloc (hipMemCreate / hipMemMap / hipMemSetAccess)", why.c_str());
-  }
-  std::lock_guard<std::mutex> lock(g_vmm_mu);
-  for (int i = 0; i < k; ++i) {
-    *outs[i] = static_cast<Elem*>(b[i].base);
-    g_vmm.push_back(std::move(b[i]));
-  }
-  return LSB_OK;
-}
-
-int rec_alloc(const lsb_ctx* c, Elem** out, size_t count) {
-  Elem** const outs[1] = {out};
-  return rec_alloc_group(c, outs, 1, count);
-}
-
-void rec_free(void* p) {
-  if (!p) return;
-  VmmBuffer b;
-  {
-    std::lock_guard<std::mutex> lock(g_vmm_mu);
-    for (size_t i = 0; i < g_vmm.size(); ++i)
-      if (g_vmm[i].base == p) {
-        b = std::move(g_vmm[i]);
-        g_vmm.erase(g_vmm.begin() + (long)i);
-        break;
-      }
-  }
-  if (!b.base) {
-    (void)hipFree(p);
-    return;
-  }
-  vmm_release(b, b.piece);
-}
-
-// ---- record buffers A and B: the optional placement probe -----------------------
-// Before round 5 the record buffers were hipMalloc'd, and how fast an LSD pass
-// streamed between two of them depended on where the driver placed them: the
-// pass ran at 6.7-7.3 ms between pairs allocated in one process
-// (profiles/r04/v5_pick.log).  Round 4 therefore chose A and B among 8
-// candidate buffers by timing one k_onesweep pass between every ordered pair
-// (~0.7 s and 128 GiB at context creation at 2^30 records).  Buffers built
-// from 1 GiB VMM pieces (rec_alloc) run every pass at 6.69-6.71 ms on average
-// in each of five fresh processes with no probe, where hipMalloc'd pairs ran
-// at 6.71, 6.99 and 7.27 (profiles/r05/alloc_sweep.log), so the probe is now
-// opt-in: LSB_PLACEMENT_CANDIDATES = K > 2 (at most 8) still tries K
-// candidates for A and B (and min(K, 3) for R), for buffers of at least
-// 1 GiB, as many as fit in 90 % of the free memory, and never when another
-// rank of this context shares the device (its timings would be the other
-// rank's too, and the candidates its memory).
-namespace {
-
-// How many candidate buffers of `bytes` to try, at most `cap` (<= 2: no probing).
-int placement_candidates(double bytes, int cap) {
-  int K = 0;
-  if (const char* e = getenv("LSB_PLACEMENT_CANDIDATES")) K = atoi(e);
-  K = std::min(K, cap);
-  size_t free_b = 0, total_b = 0;
-  if (K > 2 && bytes >= (double)(1ull << 30) && hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
-    while (K > 2 && K * bytes > 0.9 * (double)free_b) --K;
-  } else {
-    (void)hipGetLastError();
-    K = 2;
-  }
-  return K;
-}
-
-// Events of the placement probe on the rank's stream.
-struct Prober {
-  hipStream_t s;
-  int64_t m;
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  hipError_t err = hipSuccess;
-  Prober(hipStream_t s_, int64_t m_) : s(s_), m(m_) {
-    err = hipEventCreate(&e0);
-    if (err == hipSuccess) err = hipEventCreate(&e1);
-  }
-  ~Prober() {
-    if (e0) (void)hipEventDestroy(e0);
-    if (e1) (void)hipEventDestroy(e1);
-  }
-};
-
-// Up to K buffers of per records (at least `need`).
-int alloc_candidates(const lsb_ctx* c, size_t per, int K, size_t need, std::vector<Elem*>& cand) {
-  cand.clear();
-  for (int k = 0; k < K; ++k) {
-    Elem* p = nullptr;
-    if (rec_alloc(c, &p, per) != LSB_OK) break;  // fewer candidates than hoped
-    cand.push_back(p);
-  }
-  (void)hipGetLastError();
-  if (cand.size() >= need) return LSB_OK;
-  for (Elem* p : cand) rec_free(p);
-  cand.clear();
-  return fail(LSB_ERR_NOMEM, "alloc_candidates", "record buffers");
-}
-
-}  // namespace
-
-// Times one k_onesweep pass x -> y over the rank's here records on the byte
-// at `shift`, with the rank's own look-back rows and histograms
-// (onesweep_ensure); the histogram read before it is not timed.
-// hist: kOnesweepSubs * 256 u32 of scratch (r.os_hist at creation; a buffer
-// of its own once a sort may hold a histogram in r.os_hist).
-double time_pass(Rank& r, Prober& pr, const Elem* x, Elem* y, int shift, uint32_t* hist) {
-  if (pr.err != hipSuccess) return 0.0;
-  pr.err = lsb::launch_subhist(x, r.here, shift, r.os_grid, hist, nullptr, r.stream);
-  uint32_t epoch = r.os_epoch + 1;
-  if (epoch >= (1u << 30)) epoch = 2;  // as onesweep_launch: keep the parity alternation
-  if (pr.err == hipSuccess) pr.err = hipEventRecord(pr.e0, r.stream);
-  lsb::OnesweepExtra probe;
-  probe.probe = true;  // k_onesweep_probe: the same pass under its own name (profiles)
-  if (pr.err == hipSuccess)
-    pr.err = lsb::launch_onesweep(x, y, r.here, shift, -1, hist, nullptr, r.os_status, r.os_ctr, epoch,
-                                  r.os_ctr + lsb::kOnesweepSubs, r.os_grid, r.stream, probe);
-  if (pr.err == hipSuccess) r.os_epoch = epoch;
-  if (pr.err == hipSuccess) pr.err = hipEventRecord(pr.e1, r.stream);
-  if (pr.err == hipSuccess) pr.err = hipEventSynchronize(pr.e1);
-  float t = 0.f;
-  if (pr.err == hipSuccess) pr.err = hipEventElapsedTime(&t, pr.e0, pr.e1);
-  return t;
-}
-
-// A and B.  The probe is the pass itself: each candidate gets uniform PCG
-// keys, and one k_onesweep pass is timed between every ordered pair (on a
-// byte the source is not ordered by).  A copy with the same write pattern
-// (tools/kbench/allocbw.hip) ranked the buffers by their streaming write speed, but
-// that did not predict the pass, whose tile loads sit on its look-back chain
-// (profiles/r04/placement_*.log, pick.log).
-// After a probe: a probe pass that gave up on its look-back leaves the sort's
-// give-up word set and its status rows of an older parity.  Start them over
-// (as onesweep_check does) and fail the creation rather than hand the next
-// sort a false error.
-int probe_check(Rank& r) {
-  uint32_t w = 0;
-  HIP_TRY(hipMemcpy(&w, r.os_ctr + lsb::kOnesweepSubs, sizeof w, hipMemcpyDeviceToHost));
-  if (w == 0) return LSB_OK;
-  HIP_TRY(hipMemset(r.os_ctr + lsb::kOnesweepSubs, 0, sizeof(uint32_t)));
-  HIP_TRY(hipMemset(r.os_status, 0, (size_t)lsb::onesweep_tiles(r.here) * lsb::kBuckets * sizeof(uint32_t)));
-  r.os_epoch = 0;
-  return fail(LSB_ERR_HIP, "placement probe", "k_onesweep look-back timed out");
-}
-
-int alloc_records(lsb_ctx* c, Rank& r) {
-  const size_t per = (size_t)c->per;
-  int K = c->shared_device ? 0 : placement_candidates((double)per * sizeof(Elem), 8);
-  r.placement_k = 0;
-  if (K <= 2 || r.here < (int64_t)lsb::kTile * lsb::kOnesweepSubs || r.here > lsb::kOnesweepMaxElems) {
-    // LSB_ALLOC_R_EARLY=1 (experiment): R with A and B, at creation
-    const char* early = getenv("LSB_ALLOC_R_EARLY");
-    Elem** const outs[3] = {&r.A, &r.B, &r.R};
-    return rec_alloc_group(c, outs, early && atoi(early) ? 3 : 2, per);
-  }
-  std::vector<Elem*> cand;
-  LSB_TRY(alloc_candidates(c, per, K, 2, cand));
-  K = (int)cand.size();
-  auto give_up = [&](int rc) {
-    for (Elem* p : cand) rec_free(p);
-    return rc;
-  };
-  int rc = onesweep_ensure(r);
-  if (rc != LSB_OK) return give_up(rc);
-  std::vector<double> ms((size_t)K * K, 0.0);
-  std::vector<int> sorted_by(K, -8);
-  Prober pr(r.stream, r.here);
-  for (int k = 0; k < K && pr.err == hipSuccess; ++k)
-    pr.err = lsb::launch_pcg_fill(cand[k], r.here, 0x5eed + (uint64_t)k, 0, lsb::KeyGen(), r.stream);
-  (void)time_pass(r, pr, cand[0], cand[1], 0, r.os_hist);  // warm-up
-  sorted_by[1] = 0;
-  for (int x = 0; x < K; ++x)
-    for (int y = 0; y < K; ++y) {
-      if (x == y) continue;
-      const int shift = (sorted_by[x] + 8) & 63;
-      ms[(size_t)x * K + y] = time_pass(r, pr, cand[x], cand[y], shift, r.os_hist);
-      sorted_by[y] = shift;
-    }
-  if (pr.err != hipSuccess) return give_up(fail(LSB_ERR_HIP, "alloc_records: placement probe", hipGetErrorString(pr.err)));
-  rc = probe_check(r);
-  if (rc != LSB_OK) return give_up(rc);
-  // LSB_PLACEMENT_PICK=worst keeps the slowest pair instead (experiments:
-  // tools/alloc_probe.py checks that the probe predicts the passes).
-  const char* pick = getenv("LSB_PLACEMENT_PICK");
-  const bool pick_worst = pick && strcmp(pick, "worst") == 0;
-  int bx = 0, by = 1, wx = 0, wy = 1;
-  double best = 1e300, worst = 0.0;
-  for (int x = 0; x < K; ++x)
-    for (int y = x + 1; y < K; ++y) {
-      const double pair = 0.5 * (ms[(size_t)x * K + y] + ms[(size_t)y * K + x]);
-      if (pair < best) {
-        best = pair;
-        bx = x;
-        by = y;
-      }
-      if (pair > worst) {
-        worst = pair;
-        wx = x;
-        wy = y;
-      }
-    }
-  if (pick_worst) {
-    bx = wx;
-    by = wy;
-  }
-  r.placement_k = K;
-  r.placement_ms[0] = pick_worst ? worst : best;
-  r.placement_ms[1] = 0.5 * (ms[1] + ms[(size_t)K]);  // the first two buffers allocated
-  r.placement_ms[2] = worst;
-  r.A = cand[bx];
-  r.B = cand[by];
-  for (Elem* p : cand)
-    if (p != r.A && p != r.B) rec_free(p);
-  return LSB_OK;
-}
-
-// The third record buffer R (receive buffer of the exchanges, the hybrid's
-// third pass buffer), placed like A and B: among up to 3 candidates, the one
-// whose timed passes to and from B (scratch whenever R is first needed:
-// before a hybrid sort, at an exchange before its placement) take least time.
-// A may hold records by then and is not touched; the probe counts into a
-// histogram of its own, since a sort may hold one in r.os_hist.
-int alloc_third(lsb_ctx* c, Rank& r) {
-  const size_t per = (size_t)c->per;
-  int K = r.placement_k > 0 ? placement_candidates((double)per * sizeof(Elem), 3) : 1;  // probed A and B only
-  if (K <= 2) K = 1;
-  if (K == 1 || !r.os_status) return rec_alloc(c, &r.R, per);
-  std::vector<Elem*> cand;
-  LSB_TRY(alloc_candidates(c, per, K, 1, cand));
-  K = (int)cand.size();
-  uint32_t* hist = nullptr;
-  int rc = K > 1 ? dev_alloc(&hist, (size_t)lsb::kOnesweepSubs * lsb::kBuckets) : LSB_OK;
-  Prober pr(r.stream, r.here);
-  int bk = 0;
-  double best = 1e300;
-  for (int k = 0; k < K && K > 1 && rc == LSB_OK; ++k) {
-    if (pr.err == hipSuccess)
-      pr.err = lsb::launch_pcg_fill(cand[k], r.here, 0x5eed + 16 + (uint64_t)k, 0, lsb::KeyGen(), r.stream);
-    const double t = time_pass(r, pr, cand[k], r.B, 0, hist) + time_pass(r, pr, r.B, cand[k], 8, hist);
-    if (t < best) {
-      best = t;
-      bk = k;
-    }
-  }
-  (void)hipFree(hist);
-  if (rc == LSB_OK && pr.err != hipSuccess) rc = fail(LSB_ERR_HIP, "alloc_third: placement probe", hipGetErrorString(pr.err));
-  if (rc == LSB_OK && K > 1) rc = probe_check(r);
-  if (rc != LSB_OK) {
-    for (Elem* p : cand) rec_free(p);
-    return rc;
-  }
-  r.R = cand[bk];
-  for (Elem* p : cand)
-    if (p != r.R) rec_free(p);
-  return LSB_OK;
 }
 
 int init_rank(lsb_ctx* c, Rank& r, int rank, int dev) {

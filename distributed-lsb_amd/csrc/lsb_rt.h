@@ -2,6 +2,7 @@
 // state, error and timing helpers, and every function the runtime's
 // translation units share.  Not part of the C ABI.
 //
+//   lsb_alloc.cpp     record buffers (VMM pieces) and the optional placement probe
 //   lsb_context.cpp   context / rank buffers, timing, host collectives
 //   lsb_passes.cpp    the local pass driver: reduce-then-scan passes,
 //                     single-read passes (k_subhist + k_onesweep), the hybrid
@@ -266,7 +267,7 @@ int host_alloc(T** p, size_t count) {
   return LSB_OK;
 }
 
-// ---- context and rank buffers (lsb_context.cpp) -------------------------------
+// ---- record buffers (lsb_alloc.cpp) and rank buffers (lsb_context.cpp) ---------
 // Record buffers (A, B, R, candidates): VMM-backed in 1 GiB pieces when at
 // least one piece long, else hipMalloc; rec_free frees either kind.
 int rec_alloc(const lsb_ctx* c, Elem** p, size_t count);
