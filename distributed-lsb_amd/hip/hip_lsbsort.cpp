@@ -32,6 +32,12 @@
 //              RCCL "host" (NCCL_HOSTID), so RCCL links ranks that share a GPU
 //              by its socket transport -- a rehearsal of the multi-GPU path on
 //              fewer GPUs (RCCL refuses two ranks of one host on one device)
+//   --shmem    the lines and semantics of shmem/shmem_lsbsort.cpp's main
+//              (:474-584) instead of the MPI program's: "Total number of shmem
+//              PEs", verify on unless --no-verify, printed elements tagged
+//              "(rank r)", the check is checkSorted alone (key order within and
+//              across ranks, :180-219: "Array is sorted" / "Array is NOT
+//              sorted") and the exit status is !sorted (:583)
 #include <sys/wait.h>
 #include <unistd.h>
 
@@ -65,6 +71,7 @@ struct Options {
   int hybrid = 0;            // --hybrid 0|1|2 (LSB_OPT_HYBRID)
   int64_t test_corrupt = -1; // --test-corrupt I: overwrite sorted record I (tests the report)
   int share_gpus = 0;        // --share-gpus G: rank r on device r % G, one RCCL host per rank
+  bool shmem = false;        // --shmem: shmem_lsbsort.cpp's lines and exit status
 };
 
 void flush_output() {
@@ -101,8 +108,9 @@ struct World {
   bool is_local(int r) const { return r >= first && r < first + nlocal; }
 };
 
-// DistributedArray::print (mpi/mpi_lsbsort.cpp:171-200).
-void print_array(World& w, const char* name, int64_t n_per_rank) {
+// DistributedArray::print (mpi/mpi_lsbsort.cpp:171-200; shmem: each element
+// tagged with its rank, shmem/shmem_lsbsort.cpp:149-177).
+void print_array(World& w, const char* name, int64_t n_per_rank, bool shmem) {
   CHECK(lsb_barrier(w.ctx));
   if (w.root()) {
     if (n_per_rank * w.P >= w.n)
@@ -117,9 +125,12 @@ void print_array(World& w, const char* name, int64_t n_per_rank) {
       const int64_t here = lsb_here(w.n, w.P, r);
       const int64_t k = here < n_per_rank ? here : n_per_rank;
       CHECK(lsb_copy_out(w.ctx, r, 0, k, buf.data()));
-      for (int64_t i = 0; i < k; ++i)
-        printf("%s[%" PRId64 "] = (%016" PRIx64 ",%" PRIu64 ")\n", name, r * w.per + i,
-               buf[i].key, buf[i].val);
+      for (int64_t i = 0; i < k; ++i) {
+        printf("%s[%" PRId64 "] = (%016" PRIx64 ",%" PRIu64 ")", name, r * w.per + i, buf[i].key,
+               buf[i].val);
+        if (shmem) printf(" (rank %d)", r);
+        printf("\n");
+      }
       if (k < here) printf("...\n");
       flush_output();
     }
@@ -221,8 +232,10 @@ int run(World& w, const Options& o) {
   if (o.slices > 0) CHECK(lsb_set_option(w.ctx, LSB_OPT_EXCHANGE_SLICES, o.slices));
   if (o.hybrid > 0) CHECK(lsb_set_option(w.ctx, LSB_OPT_HYBRID, o.hybrid));
   if (w.root()) {
-    // the reference's own line (mpi/mpi_lsbsort.cpp:619): a rank here is one GPU
-    printf("Total number of MPI ranks: %d\n", w.P);
+    // the reference's own line (mpi/mpi_lsbsort.cpp:619, shmem/shmem_lsbsort.cpp:498):
+    // a rank here is one GPU
+    if (o.shmem) printf("Total number of shmem PEs: %d\n", w.P);
+    else printf("Total number of MPI ranks: %d\n", w.P);
     printf("Problem size: %" PRId64 "\n", o.n);
     flush_output();
   }
@@ -241,7 +254,7 @@ int run(World& w, const Options& o) {
     }
     CHECK(lsb_barrier(w.ctx));
   }
-  if (o.print) print_array(w, "A", 10);
+  if (o.print) print_array(w, "A", 10, o.shmem);
 
   double elapsed = 0;
   {
@@ -262,7 +275,7 @@ int run(World& w, const Options& o) {
     }
     CHECK(lsb_barrier(w.ctx));
   }
-  if (o.print) print_array(w, "A", 10);
+  if (o.print) print_array(w, "A", 10, o.shmem);
   if (o.test_corrupt >= 0 && o.test_corrupt < o.n) {
     // Test hook: overwrite one sorted record so the failure report can be checked.
     const int r = (int)(o.test_corrupt / w.per);
@@ -274,7 +287,14 @@ int run(World& w, const Options& o) {
   }
 
   int status = 0;
-  if (o.verify) {
+  if (o.verify && o.shmem) {
+    // shmem_lsbsort's check (:568-583): checkSorted only, exit status !sorted
+    int sorted = 0;
+    CHECK(lsb_check_sorted(w.ctx, &sorted));
+    if (w.root()) printf(sorted ? "Array is sorted\n" : "Array is NOT sorted\n");
+    flush_output();
+    status = sorted ? 0 : 1;
+  } else if (o.verify) {
     if (w.root()) {
       printf("Verifying\n");
       flush_output();
@@ -376,6 +396,7 @@ int main(int argc, char* argv[]) {
     else if (a == "--hybrid") o.hybrid = std::stoi(next());
     else if (a == "--test-corrupt") o.test_corrupt = std::stoll(next());
     else if (a == "--share-gpus") o.share_gpus = std::stoi(next());
+    else if (a == "--shmem") o.shmem = true;
     else if (a == "--exchange") {
       const std::string x = next();
       if (x == "alltoallv") o.exchange_option = -1;
@@ -390,7 +411,8 @@ int main(int argc, char* argv[]) {
       else { fprintf(stderr, "unknown --dist %s\n", d.c_str()); return 2; }
     }
   }
-  if (!o.verify_set) o.verify = (o.n < 128LL * 1024 * 1024);
+  // MPI: verify iff n < 128Mi (mpi/mpi_lsbsort.cpp:609-611); SHMEM: always (:479)
+  if (!o.verify_set) o.verify = o.shmem || (o.n < 128LL * 1024 * 1024);
   if (o.radix_bits == 0) o.radix_bits = o.gpus > 1 ? 16 : 8;
   if (o.n < 0 || o.ranks < 1 || o.gpus < 0 || o.share_gpus < 0 || o.hybrid < 0 || o.hybrid > 2) {
     fprintf(stderr, "invalid arguments\n");

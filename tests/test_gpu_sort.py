@@ -579,6 +579,31 @@ def test_beyond_32bit_indices(lsb_built):
 
 
 # ------------------------------------------------------------- the harness
+@pytest.mark.parametrize("corrupt", [False, True])
+def test_harness_shmem_lines(lsb_built, ref_vectors, corrupt):
+    """--shmem: the lines and exit status of shmem/shmem_lsbsort.cpp's main
+    (:474-584): its banner (:498), verify on by default (:479), printed
+    elements tagged with their rank (:149-177), checkSorted alone (:568-578)
+    and exit status !sorted (:583).  The SHMEM program itself cannot be built
+    here (no OpenSHMEM), so its print vectors are the MPI program's (same
+    input, same sorted output, same element format, :36-41) with the tag."""
+    case = next(c for c in ref_vectors["cases"] if c["n"] == 1000003 and c["P"] == 4)
+    args = [lsb_built.HARNESS_PATH, "--n", "1000003", "--ranks", "4", "--print", "--shmem"]
+    if corrupt:
+        args += ["--test-corrupt", "400000"]  # a small key in rank 1's sorted middle
+    r = subprocess.run(args, capture_output=True, text=True, timeout=300)
+    lines = r.stdout.splitlines()
+    assert lines[0] == "Total number of shmem PEs: 4" and lines[1] == "Problem size: 1000003"
+    assert "Verifying" not in lines
+    per = 250001
+    printed = [l for l in lines if l.startswith("A[")]
+    assert printed == [f"A[{i}] = ({k},{v}) (rank {i // per})" for i, k, v in case["input"] + case["output"]]
+    if corrupt:
+        assert "Array is NOT sorted" in lines and r.returncode == 1
+    else:
+        assert "Array is sorted" in lines and r.returncode == 0
+
+
 @pytest.mark.parametrize("extra", [[], ["--exchange", "peer"], ["--slices", "3", "--radix-bits", "16"],
                                    ["--radix-bits", "64"], ["--radix-bits", "64", "--hybrid", "1"],
                                    ["--radix-bits", "64", "--hybrid", "2"]])
