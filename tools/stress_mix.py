@@ -9,7 +9,8 @@ three instead sorts host-made keys (up to 2^22 records) whose bytes are
 thinned out at random -- constant bytes, few distinct values in the middle
 bytes, duplicates -- the inputs that take the hybrid's fallbacks and
 k_segfix's long crossing runs; those are checked against numpy's stable
-argsort.  Runs until --seconds have passed; one line per iteration.
+argsort.  Record buffers come from VMM pieces of a drawn size (2 MiB,
+64 MiB or the default 1 GiB), so small sorts run the VMM allocator too.  Runs until --seconds have passed; one line per iteration.
 
     python tools/stress_mix.py --seconds 240 --seed 1
 """
@@ -69,7 +70,12 @@ def main():
         if host:
             n = min(n, 1 << 22)
             dist = "thinned"
-        desc = f"iter {it}: n={n} P={P} bits={bits} dist={dist} split={split} hybrid={hybrid} gather={gather}"
+        # record buffers from VMM pieces of 2 / 64 MiB (several pieces per
+        # buffer at these sizes), or the default 1 GiB (hipMalloc below it)
+        vmm = rng.choice((2, 64, 1024, 1024))
+        os.environ["LSB_VMM_CHUNK_MIB"] = str(vmm)
+        desc = (f"iter {it}: n={n} P={P} bits={bits} dist={dist} split={split} hybrid={hybrid} "
+                f"gather={gather} vmm={vmm}")
         t0 = time.time()
         try:
             with lsbsort.World(n, ranks=P, radix_bits=bits) as w:
