@@ -8,6 +8,8 @@
 #   n2        bench.py --gpus 2 with no launcher over RCCL's socket transport
 #             (two rank processes on the one GPU: the N > 1 code path, not a speed)
 #   n4zipf    the same at N = 4 with Zipf keys
+#   n8        bench.py --gpus 8 over RCCL sockets at 2^22 records per rank (the driver's N = 8 flow)
+#   table     tools/table_runs.sh: the DESIGN.md §4 table on this box
 #   torchrun  bench.py --gpus 2 under torch.distributed.run (the driver's form)
 #   profile   tools/profile.sh: rocprofv3 stats + FETCH_SIZE / WRITE_SIZE passes
 #   profhyb   the same for bench.py --passes hybrid (gpurun_out/prof_hybrid;
@@ -48,6 +50,13 @@ for s in $RUN; do
         --n-per-gpu 16777216 --steps 2 --warmup 1 --no-cpu-baseline > $O/bench_n4_zipf.log 2>&1 \
         || fail n4zipf $O/bench_n4_zipf.log
       tail -1 $O/bench_n4_zipf.log | cut -c1-400 ;;
+    n8)  # the driver's largest N over RCCL sockets: eight rank processes on the one GPU, both extras
+      timeout -k 10 600 python -u bench.py --gpus 8 --transport rccl-sockets --n-per-gpu 4194304 \
+        --steps 2 --warmup 1 --no-cpu-baseline > $O/bench_n8.log 2>&1 || fail n8 $O/bench_n8.log
+      tail -1 $O/bench_n8.log | cut -c1-400 ;;
+    table)  # the DESIGN.md §4 table (tools/table_runs.sh)
+      TABLE=$TAG/table timeout -k 10 1100 bash tools/table_runs.sh > $O/table_summary.log 2>&1 || fail table $O/table_summary.log
+      cat $O/table_summary.log ;;
     torchrun)
       timeout -k 10 400 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
         --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --transport rccl-sockets \
