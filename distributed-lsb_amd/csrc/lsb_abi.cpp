@@ -71,10 +71,14 @@ int lsb_rank_footprint(int64_t n_total, int num_ranks, int radix_bits, int with_
   const int64_t P = num_ranks, per = div_ceil(n_total, num_ranks);
   const int64_t nb = radix_bits == 64 ? lsb::kBuckets : (int64_t)1 << radix_bits;
   const int64_t rec = rec_bytes((size_t)per);
+  const int64_t cap = record_capacity(per, (int)P);                // A and B (regional slots)
   const int64_t tiles = lsb::onesweep_tiles(per);
   const lsb::Chunking ch = lsb::make_chunking(per, 2 * 256);
-  int64_t b = 2 * rec + (with_recv ? rec : 0);
+  int64_t b = 2 * (int64_t)rec_bytes((size_t)cap) + (with_recv ? rec : 0);
   b += tiles * lsb::kBuckets * 4;                                   // os_status
+  if (region_cap_for(per, (int)P) > 0)  // os_status2 and rg_buf of the regional first pass
+    b += lsb::onesweep_tiles(region_cap_for(per, (int)P) * lsb::kRegions) * lsb::kBuckets * 4 +
+         (lsb::kRegions + 512) * 4;
   if (P > 1 || with_recv) b += tiles * (int64_t)sizeof(lsb::TileDesc) + 2 * P * nb * 8;  // gdesc, gstart
   b += (int64_t)lsb::kBuckets * std::max(1, ch.num_chunks) * 12;    // chunk_hist, chunk_off
   b += (int64_t)lsb::kBuckets * 8 + (radix_bits == 16 ? 2 * 65536 * 8 : 0);  // totals, totals16, first16
@@ -213,6 +217,9 @@ int lsb_set_option(lsb_ctx_t* c, int option, int64_t value) {
     case LSB_OPT_ONESWEEP:
       c->onesweep = value != 0;
       return LSB_OK;
+    case LSB_OPT_REGION_FIRST:
+      c->region = value != 0;
+      return LSB_OK;
     case LSB_OPT_EXCHANGE_PEER:
       c->peer = value != 0;
       return LSB_OK;
@@ -319,6 +326,7 @@ int lsb_sort(lsb_ctx_t* c) {
   const int passes = 64 / c->bits;
   c->last_local_passes = c->last_exchanges = 0;
   c->last_varying = ~0ull;
+  c->last_first = LSB_FIRST_COUNT;
   c->pass_cursor = 0;
   c->cur_pass = 0;
   if (c->bits == 64 && exchanging(c)) {
@@ -355,6 +363,13 @@ int lsb_get_last_sort(lsb_ctx_t* c, int* local_passes, int* exchanges, uint64_t*
   if (local_passes) *local_passes = c->last_local_passes;
   if (exchanges) *exchanges = c->last_exchanges;
   if (varying_bits) *varying_bits = c->last_varying;
+  return LSB_OK;
+}
+
+int lsb_get_first_pass(lsb_ctx_t* c, int* form) {
+  LSB_TRY(check_ctx(c));
+  if (!form) return fail(LSB_ERR_INVALID, "lsb_get_first_pass", "null");
+  *form = c->last_first;
   return LSB_OK;
 }
 

@@ -284,8 +284,19 @@ int probe_check(Rank& r) {
   return fail(LSB_ERR_HIP, "placement probe", "k_onesweep look-back timed out");
 }
 
+int64_t region_min() {
+  if (const char* e = getenv("LSB_REGION_MIN")) return std::max<int64_t>(atoll(e), int64_t(1) << 16);
+  return lsb::kRegionMin;
+}
+
+int64_t region_cap_for(int64_t per, int P) { return P == 1 ? lsb::region_cap(per, region_min()) : 0; }
+
+int64_t record_capacity(int64_t per, int P) { return std::max(per, region_cap_for(per, P) * lsb::kRegions); }
+
 int alloc_records(lsb_ctx* c, Rank& r) {
-  const size_t per = (size_t)c->per;
+  const size_t per = (size_t)record_capacity(c->per, c->P);
+  r.cap = (int64_t)per;
+  r.rg_cap = region_cap_for(c->per, c->P);
   int K = c->shared_device ? 0 : placement_candidates((double)per * sizeof(Elem), 8);
   r.placement_k = 0;
   if (K <= 2 || r.here < (int64_t)lsb::kTile * lsb::kOnesweepSubs || r.here > lsb::kOnesweepMaxElems) {

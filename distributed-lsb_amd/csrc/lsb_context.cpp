@@ -136,6 +136,9 @@ void free_rank(Rank& r) {
   (void)hipHostFree(r.split_h);
   (void)hipFree(r.merge_path);
   (void)hipFree(r.os_status);
+  (void)hipFree(r.os_status2);
+  (void)hipFree(r.rg_buf);
+  (void)hipHostFree(r.rg_h);
   (void)hipFree(r.gstart);
   (void)hipFree(r.gdesc);
   (void)hipFree(r.seg_base);

@@ -170,6 +170,49 @@ struct GatherSrc {
 // gadj, then desc[t] for every onesweep tile of m records (after launch_plan
 // with gstart).
 hipError_t launch_gather_desc(const GatherSrc& g, int64_t m, TileDesc* desc, hipStream_t s);
+// Regional first pass (P == 1 LSD sorts of at least kRegionMin records,
+// LSB_OPT_REGION_FIRST): the sort's first pass needs no
+// histogram read.  Its records of digit b from sub-array x go to region
+// r = b * kOnesweepSubs + x of the output, a slot range of `cap` records
+// (a multiple of kTile, with slack over the mean region_mean(m)): slot
+// r * cap + (the record's rank among them, from the look-back alone).  The
+// output then holds the records in the stable order of that digit, with a
+// gap at the end of every region, and the second pass reads it tile by tile,
+// taking counts[r] records of each region (its tiles of kTile slots:
+// the valid prefix of each).  A region that would overflow sets *ovf (the
+// output is invalid and the runtime sorts the kept input the usual way).
+// Mode 1 (the first pass, next digit counted over the regional layout's
+// tiles): counts[r] accumulated here (zeroed by the launcher).  Mode 2 (the
+// second pass): reads that layout, writes a dense one.  No key span: the
+// runtime takes the form only when a sample shows every byte varying.
+constexpr int64_t kRegionMin = int64_t(1) << 27;
+constexpr int kRegions = kBuckets * kOnesweepSubs;  // 2048
+inline int64_t region_mean(int64_t m) { return (m + kRegions - 1) / kRegions; }
+// Slots per region for m records (0: fewer than min_m records, too few for
+// the form): the mean plus max(mean / 64, 16 standard deviations of a
+// uniform region's count), rounded up to whole tiles.  2^27 records: +6.25 %
+// slots; 2^30: +2.3 %.  (Tests lower min_m to cover small sorts, whose
+// regions are then one mostly empty tile each.)
+inline int64_t region_cap(int64_t m, int64_t min_m = kRegionMin) {
+  if (m < min_m || m <= 0) return 0;
+  const int64_t mu = region_mean(m);
+  int64_t sd = 1;
+  while (sd * sd < mu) ++sd;
+  const int64_t slack = mu / 64 > 16 * sd ? mu / 64 : 16 * sd;
+  return (mu + slack + kTile - 1) / kTile * kTile;
+}
+inline int64_t region_slots(int64_t m, int64_t min_m = kRegionMin) { return region_cap(m, min_m) * kRegions; }
+struct RegionPass {
+  int64_t cap = 0;                    // slots per region
+  uint32_t* counts = nullptr;         // [kRegions] records per region
+  uint32_t* ovf = nullptr;            // mode 1: set when a region overflows
+};
+// Sample of the sort's first digit (the regional first pass's go / no-go):
+// 256 workgroups read one tile each, spread over the m records; hist[256]
+// (zeroed here) gets the tiles' digit counts at `shift`, span[2] (zeroed
+// here) the OR of their keys and complements.
+hipError_t launch_sample(const Elem* A, int64_t m, int shift, uint32_t* hist, uint64_t* span,
+                         hipStream_t s);
 struct OnesweepExtra {
   uint64_t* totals = nullptr;
   uint64_t* count16 = nullptr;
@@ -177,6 +220,8 @@ struct OnesweepExtra {
   const SegPass* seg = nullptr;  // the hybrid's last pass (no next digit, whole stage)
   const GatherSrc* gather = nullptr;  // records gathered from an exchange (`in` unused)
   bool probe = false;  // the placement probe's pass (a last pass, launched as k_onesweep_probe)
+  const RegionPass* region = nullptr;  // with region_mode 1 or 2: the regional layout
+  int region_mode = 0;  // 1: write it (needs a next digit); 2: read it (sub_hist over its tiles)
 };
 // The runtime's choice of OnesweepExtra::halves for a rank, from a digit's
 // sub-array histogram (kOnesweepSubs x 256 counts of m records): 2 when one

@@ -736,6 +736,44 @@ __global__ __launch_bounds__(BLOCK) void k_subhist(const Elem* __restrict__ A, i
   }
 }
 
+// The regional first pass's sample (launch_sample): workgroup g reads tile
+// floor(g * TT / G) of A, 16 records per thread.
+constexpr int kSampleBlock = 256;
+constexpr int kSampleTiles = 256;
+__global__ __launch_bounds__(kSampleBlock) void k_sample(const Elem* __restrict__ A, int64_t m, int shift,
+                                                         uint32_t* __restrict__ hist,
+                                                         unsigned long long* __restrict__ span) {
+  constexpr int IPT = kTile / kSampleBlock;
+  __shared__ uint32_t h[kBuckets];
+  h[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t TT = (m + kTile - 1) / kTile;
+  const int64_t tb = (int64_t)blockIdx.x * TT / gridDim.x * kTile;
+  const uint64_t* __restrict__ keys = reinterpret_cast<const uint64_t*>(A);
+  uint64_t kor = 0, knor = 0;
+#pragma unroll
+  for (int i = 0; i < IPT; ++i) {
+    const int64_t idx = tb + (int64_t)i * kSampleBlock + threadIdx.x;
+    if (idx < m) {
+      const uint64_t k = __builtin_nontemporal_load(keys + 2 * idx);
+      kor |= k;
+      knor |= ~k;
+      atomicAdd(&h[(uint32_t)(k >> shift) & (kBuckets - 1)], 1u);
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    kor |= __shfl_xor(kor, off, 64);
+    knor |= __shfl_xor(knor, off, 64);
+  }
+  if (lane_id() == 0) {
+    atomicOr(&span[0], (unsigned long long)kor);
+    atomicOr(&span[1], (unsigned long long)knor);
+  }
+  __syncthreads();
+  if (h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
+}
+
 // Phase timing (profiling build, -DLSB_OS_PROFILE): thread 0 of every
 // workgroup adds s_memtime deltas between the barriers of a tile into
 // g_os_prof[phase]; the runtime prints them at lsb_destroy.
@@ -794,16 +832,24 @@ __device__ unsigned long long g_os_prof[10];
 // copy.  Wave 0 fetches the next tile's TileDesc while this tile is written,
 // so the loads at the loop top wait on nothing new; a tile of more than
 // kDescPieces pieces searches the piece table per record.
-template <int BLOCK, int IPT, bool NEXT, bool C16, int HALVES, bool SEG, bool GATHER>
+//
+// RG (the regional first pass, RegionPass in lsb_kernels.h): RG = 1 is a
+// sort's first pass without a histogram: bucket b's run of a tile of
+// sub-array x starts at region (b, x)'s first slot plus the look-back sum,
+// and the next digit is counted over the regional layout's tiles.  RG = 2
+// reads that layout: tile t takes the valid prefix of its region's slots.
+template <int BLOCK, int IPT, bool NEXT, bool C16, int HALVES, bool SEG, bool GATHER, int RG>
 __device__ __forceinline__ void onesweep_body(
     const Elem* __restrict__ in, Elem* __restrict__ out, int64_t m, int shift, int next_shift,
     const uint32_t* __restrict__ sub_hist, uint32_t* __restrict__ next_hist,
     uint32_t* __restrict__ status, uint32_t* __restrict__ tile_ctr, uint32_t epoch,
     uint32_t* __restrict__ err, uint64_t* __restrict__ totals,
-    unsigned long long* __restrict__ count16, SegPass seg, GatherSrc gs) {
+    unsigned long long* __restrict__ count16, SegPass seg, GatherSrc gs, RegionPass rg) {
   constexpr int W = BLOCK / 64;
   constexpr int T = BLOCK * IPT;
   static_assert(!SEG || (!NEXT && !C16 && HALVES == 1), "the segment pass: last pass, whole stage");
+  static_assert(RG == 0 || (!C16 && HALVES == 1 && !SEG && !GATHER), "regional passes: plain whole stage");
+  static_assert(RG != 1 || NEXT, "the regional first pass counts the next digit");
   // Thread t < 256 owns bucket t (counts, scan, look-back, offsets); with
   // BLOCK = 512 the other threads only load, rank, stage and write.
   static_assert(BLOCK % kBuckets == 0, "bucket threads");
@@ -819,7 +865,7 @@ __device__ __forceinline__ void onesweep_body(
   __shared__ uint32_t nh[NEXT ? kSub * kBuckets : 1];  // next digit's sub-array histogram
   __shared__ uint64_t scan64[W];
   __shared__ uint32_t scan32[W];
-  __shared__ int32_t s_tile, s_sub;
+  __shared__ int32_t s_tile, s_sub, s_nv;
   __shared__ uint32_t tile_lo[2];  // C16: low byte of the tile's first, last record
   __shared__ TileDesc s_desc;      // GATHER: where this tile's records are
 
@@ -827,7 +873,13 @@ __device__ __forceinline__ void onesweep_body(
   const bool bkt = BLOCK == kBuckets || t < kBuckets;  // a bucket thread
   const int w = t >> 6;
   const uint32_t lane = lane_id();
-  const int64_t TT = (m + T - 1) / T;
+  // Tiles of this pass's input (TT) and of the next pass's (TTn: its
+  // sub-arrays are what the next digit is counted by); output slots (mcap).
+  const int64_t slots = RG != 0 ? rg.cap * kRegions : m;
+  const int64_t TT = RG == 2 ? slots / T : (m + T - 1) / T;
+  const int64_t TTn = RG == 1 ? slots / T : (m + T - 1) / T;
+  const int64_t mcap = RG == 1 ? slots : m;
+  uint32_t racc = 0;                     // RG = 1: thread t's count of region (t, cur_sub)
   // Granule tags (bits 30-31): this launch's parity, and the prefix bit.
   constexpr uint32_t kValMask = kStatusValMask, kPreBit = 1u << 30;
   const uint32_t tag_agg = (epoch & 1u) << 31, tag_pre = tag_agg | kPreBit;
@@ -847,7 +899,7 @@ __device__ __forceinline__ void onesweep_body(
   uint64_t tot = 0;
 #pragma unroll
   for (int x = 0; x < kSub; ++x) {
-    const uint32_t v = bkt ? sub_hist[x * kBuckets + t] : 0u;
+    const uint32_t v = bkt && RG != 1 ? sub_hist[x * kBuckets + t] : 0u;
     if (HALVES == 1) col[x] = v;
     tot += v;
   }
@@ -901,7 +953,21 @@ __device__ __forceinline__ void onesweep_body(
   // The next tile's id is fetched while this tile's records are written
   // (a device-scope atomic is ~1 us under load; 3 % of the sort, measured).
   int nxt_tile = -1, nxt_sub = 0;
-  if (t == 0) grab(nxt_tile, nxt_sub);
+  // RG = 2: thread 0 also reads the next tile's valid count (tile k of region
+  // r holds that region's slots [k * T, (k + 1) * T)) while this tile is
+  // written, so the loads at the loop top wait on nothing new.
+  int nxt_nv = 0;
+  auto region_nvalid = [&](int tl) -> int {
+    if (tl < 0) return 0;
+    const uint32_t ct = (uint32_t)(rg.cap / T);
+    const uint32_t reg = (uint32_t)tl / ct;
+    const int64_t v = (int64_t)rg.counts[reg] - (int64_t)((uint32_t)tl - reg * ct) * T;
+    return (int)(v < 0 ? 0 : (v < T ? v : T));
+  };
+  if (t == 0) {
+    grab(nxt_tile, nxt_sub);
+    if (RG == 2) nxt_nv = region_nvalid(nxt_tile);
+  }
   // GATHER: lanes 0-3 of wave 0 hold the next tile's descriptor.
   uint4 dreg = make_uint4(0u, 0u, 0u, 0u);
   auto fetch_desc = [&]() {
@@ -916,6 +982,7 @@ __device__ __forceinline__ void onesweep_body(
     if (t == 0) {
       s_tile = nxt_tile;
       s_sub = nxt_sub;
+      if (RG == 2) s_nv = nxt_nv;
     }
     if (GATHER && w == 0 && lane < 4) reinterpret_cast<uint4*>(&s_desc)[lane] = dreg;
 #pragma unroll
@@ -926,15 +993,21 @@ __device__ __forceinline__ void onesweep_body(
     if (tile < 0) break;
     const int x = s_sub;
     if (x != cur_sub) {
-      cur_sub = x;
-      uint64_t pre = 0;
+      if (RG == 1) {
+        if (bkt && cur_sub >= 0 && racc) atomicAdd(&rg.counts[t * kSub + cur_sub], racc);
+        racc = 0;
+        base = (uint64_t)((bkt ? t : 0) * kSub + x) * (uint64_t)rg.cap;  // region (t, x)
+      } else {
+        uint64_t pre = 0;
 #pragma unroll
-      for (int xx = 0; xx < kSub; ++xx)
-        pre += xx < x ? (HALVES == 1 ? col[xx] : (bkt ? sub_hist[xx * kBuckets + t] : 0u)) : 0u;
-      base = bstart + pre;
+        for (int xx = 0; xx < kSub; ++xx)
+          pre += xx < x ? (HALVES == 1 ? col[xx] : (bkt ? sub_hist[xx * kBuckets + t] : 0u)) : 0u;
+        base = bstart + pre;
+      }
+      cur_sub = x;
     }
     const int64_t tb = (int64_t)tile * T;
-    const int nvalid = (int)((m - tb) < T ? (m - tb) : T);
+    const int nvalid = RG == 2 ? s_nv : (int)((m - tb) < T ? (m - tb) : T);
 
     Elem e[IPT];
     const int wbase = w * 64 * IPT + (int)lane;
@@ -1054,6 +1127,7 @@ __device__ __forceinline__ void onesweep_body(
         wcnt[ww][t] = (WC)cnt;
         cnt += v;
       }
+      if (RG == 1) racc += cnt;
     }
     bool mixed16 = false;
     if (C16) {
@@ -1141,7 +1215,13 @@ __device__ __forceinline__ void onesweep_body(
     }
     const uint32_t eb_left = pair_swap(eb);  // odd lanes: lane t - 1's sum
     const uint64_t excl = even ? ea : eb_left;
-    const int64_t R = (int64_t)(base + excl);  // first output slot of the run
+    int64_t R = (int64_t)(base + excl);  // first output slot of the run
+    if (RG == 1 && bkt && excl + cnt > (uint64_t)rg.cap) {
+      // Region (t, x) overflows: the output is invalid (the runtime redoes
+      // the sort from the kept input); keep the run inside the buffer.
+      atomicOr(rg.ovf, 1u);
+      R = R < mcap - (int64_t)cnt ? R : mcap - (int64_t)cnt;
+    }
     if (bkt) delta[t] = R - (int64_t)lstart;
     if (NEXT && bkt) {
       // The run [R, R + cnt) lies in next-pass sub-array x0, except from
@@ -1149,10 +1229,10 @@ __device__ __forceinline__ void onesweep_body(
       // most one: a non-empty sub-array holds >= kTile records).
       uint32_t c = 0xFFFFu;  // jb = 0xFFFF: never
       if (cnt > 0) {
-        const int x0 = sub_of_tile(R / T, TT);
-        const int64_t bnd = x0 + 1 < kSub ? sub_first_tile(x0 + 1, TT) * T : m;
+        const int x0 = sub_of_tile(R / T, TTn);
+        const int64_t bnd = x0 + 1 < kSub ? sub_first_tile(x0 + 1, TTn) * T : mcap;
         if (R + cnt > bnd) {
-          const int x1 = sub_of_tile(bnd / T, TT);
+          const int x1 = sub_of_tile(bnd / T, TTn);
           c = (uint32_t)(lstart + (bnd - R)) | ((uint32_t)x0 << 16) | ((uint32_t)x1 << 24);
         } else {
           c = 0xFFFFu | ((uint32_t)x0 << 16) | ((uint32_t)x0 << 24);
@@ -1165,18 +1245,21 @@ __device__ __forceinline__ void onesweep_body(
 #ifdef LSB_OS_PROFILE
     if (t == 0) ++prof[8];
 #endif
-    if (t == 0) grab(nxt_tile, nxt_sub);  // in flight during the writes
+    if (t == 0) {  // in flight during the writes
+      grab(nxt_tile, nxt_sub);
+      if (RG == 2) nxt_nv = region_nvalid(nxt_tile);
+    }
 
     // emit: one staged record (tile position j, output slot delta + pos) to
     // memory, and its next digit to the sub-array histogram.
     // g = delta[digit] + the record's slot in its run, c = cut[digit].
     auto emit = [&](auto skew_tag, const Elem& v, int j, int64_t g, uint32_t c) {
       constexpr bool kSkew = decltype(skew_tag)::value;
-      LSB_DASSERT(g >= 0 && g < m);
+      LSB_DASSERT(g >= 0 && g < mcap);
       // In range by construction.  The clamp keeps a look-back that gave up
       // (err set, output reported invalid) from storing outside `out`; a
       // clamp, not a branch: the conditional store cost 6 % of the sort.
-      const uint64_t gs = (uint64_t)g < (uint64_t)(m - 1) ? (uint64_t)g : (uint64_t)(m - 1);
+      const uint64_t gs = (uint64_t)g < (uint64_t)(mcap - 1) ? (uint64_t)g : (uint64_t)(mcap - 1);
       store_elem(out + gs, v);
       if (NEXT) {
         const uint32_t xs = (uint32_t)j >= (c & 0xFFFFu) ? (c >> 24) : ((c >> 16) & 0xFFu);
@@ -1327,17 +1410,19 @@ __device__ __forceinline__ void onesweep_body(
     for (int i = t; i < kSub * kBuckets; i += BLOCK)
       if (nh[i]) atomicAdd(&next_hist[i], nh[i]);
   }
+  if (RG == 1 && bkt && cur_sub >= 0 && racc) atomicAdd(&rg.counts[t * kSub + cur_sub], racc);
 }
 
-template <int BLOCK, int IPT, bool NEXT, bool C16, int HALVES, bool SEG = false, bool GATHER = false>
+template <int BLOCK, int IPT, bool NEXT, bool C16, int HALVES, bool SEG = false, bool GATHER = false, int RG = 0>
 __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_onesweep(
     const Elem* __restrict__ in, Elem* __restrict__ out, int64_t m, int shift, int next_shift,
     const uint32_t* __restrict__ sub_hist, uint32_t* __restrict__ next_hist,
     uint32_t* __restrict__ status, uint32_t* __restrict__ tile_ctr, uint32_t epoch,
     uint32_t* __restrict__ err, uint64_t* __restrict__ totals,
-    unsigned long long* __restrict__ count16, SegPass seg, GatherSrc gs) {
-  onesweep_body<BLOCK, IPT, NEXT, C16, HALVES, SEG, GATHER>(in, out, m, shift, next_shift, sub_hist, next_hist,
-                                                            status, tile_ctr, epoch, err, totals, count16, seg, gs);
+    unsigned long long* __restrict__ count16, SegPass seg, GatherSrc gs, RegionPass rg) {
+  onesweep_body<BLOCK, IPT, NEXT, C16, HALVES, SEG, GATHER, RG>(in, out, m, shift, next_shift, sub_hist,
+                                                                next_hist, status, tile_ctr, epoch, err, totals,
+                                                                count16, seg, gs, rg);
 }
 
 // The placement probe's pass (lsb_context.cpp alloc_records): the same code
@@ -1350,9 +1435,9 @@ __global__ __launch_bounds__(kOsBlock, 2 * kOsBlock / 256) void k_onesweep_probe
     uint32_t* __restrict__ status, uint32_t* __restrict__ tile_ctr, uint32_t epoch,
     uint32_t* __restrict__ err, uint64_t* __restrict__ totals,
     unsigned long long* __restrict__ count16, SegPass seg, GatherSrc gs) {
-  onesweep_body<kOsBlock, kOsIpt, false, false, 1, false, false>(in, out, m, shift, next_shift, sub_hist,
-                                                                 next_hist, status, tile_ctr, epoch, err,
-                                                                 totals, count16, seg, gs);
+  onesweep_body<kOsBlock, kOsIpt, false, false, 1, false, false, 0>(in, out, m, shift, next_shift, sub_hist,
+                                                                    next_hist, status, tile_ctr, epoch, err,
+                                                                    totals, count16, seg, gs, RegionPass());
 }
 
 // ------------------------------------------------------------------- place
@@ -1955,6 +2040,18 @@ hipError_t launch_subhist(const Elem* A, int64_t m, int shift, int grid, uint32_
   return hipGetLastError();
 }
 
+hipError_t launch_sample(const Elem* A, int64_t m, int shift, uint32_t* hist, uint64_t* span, hipStream_t s) {
+  if (shift < 0 || shift > 56) return hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(hist, 0, sizeof(uint32_t) * kBuckets, s);
+  if (e == hipSuccess) e = hipMemsetAsync(span, 0, 2 * sizeof(uint64_t), s);
+  if (e != hipSuccess || m <= 0) return e;
+  const int64_t TT = (m + kTile - 1) / kTile;
+  const unsigned g = (unsigned)(TT < kSampleTiles ? TT : kSampleTiles);
+  hipLaunchKernelGGL(k_sample, dim3(g), dim3(kSampleBlock), 0, s, A, m, shift, hist,
+                     reinterpret_cast<unsigned long long*>(span));
+  return hipGetLastError();
+}
+
 int onesweep_halves_for(const uint32_t* h, int64_t m) {
   for (int b = 0; b < kBuckets; ++b) {
     uint64_t tot = 0;
@@ -1976,7 +2073,13 @@ hipError_t launch_onesweep(const Elem* in, Elem* out, int64_t m, int shift, int 
     return hipErrorInvalidValue;
   hipError_t e = hipMemsetAsync(tile_ctr, 0, sizeof(uint32_t) * kSub, s);
   if (e != hipSuccess) return e;
-  const int64_t TT = (m + kTile - 1) / kTile;
+  const int rm = extra.region_mode;
+  const RegionPass rp = extra.region ? *extra.region : RegionPass();
+  if (rm < 0 || rm > 2 || (rm != 0 && (!extra.region || rp.cap <= 0 || rp.cap % kTile != 0 ||
+                                       rp.cap * kRegions < m || !rp.counts)))
+    return hipErrorInvalidValue;
+  // Tiles of the input: the regional layout's slots for its reading pass.
+  const int64_t TT = rm == 2 ? rp.cap * kRegions / kTile : (m + kTile - 1) / kTile;
   auto* c16 = reinterpret_cast<unsigned long long*>(extra.count16);
   const bool gat = extra.gather != nullptr;
   // The split stage only for the plain and next-digit forms, never gathered
@@ -1996,9 +2099,34 @@ hipError_t launch_onesweep(const Elem* in, Elem* out, int64_t m, int shift, int 
   auto go = [&](auto kplain, auto kgather, int nshift, uint32_t* nhist, unsigned long long* cnt16,
                 SegPass sp) {
     hipLaunchKernelGGL(gat ? kgather : kplain, gd, bd, 0, s, in, out, m, shift, nshift, sub_hist, nhist,
-                       st, tile_ctr, epoch, err, extra.totals, cnt16, sp, gsrc);
+                       st, tile_ctr, epoch, err, extra.totals, cnt16, sp, gsrc, RegionPass());
   };
-  if (extra.probe) {
+  if (rm != 0) {
+    // The regional first pass (rm = 1) and the pass that reads its layout
+    // (rm = 2): whole stage, no 16-bit counts, totals, segments or gathering.
+    if (c16 || extra.halves != 1 || extra.seg || gat || extra.probe || extra.totals) return hipErrorInvalidValue;
+    if (rm == 1 && (next_shift < 0 || !rp.ovf)) return hipErrorInvalidValue;
+    if (next_shift >= 0) {
+      e = hipMemsetAsync(next_hist, 0, sizeof(uint32_t) * kSub * kBuckets, s);
+      if (e != hipSuccess) return e;
+    }
+    if (rm == 1) {
+      e = hipMemsetAsync(rp.counts, 0, sizeof(uint32_t) * kRegions, s);
+      if (e == hipSuccess) e = hipMemsetAsync(rp.ovf, 0, sizeof(uint32_t), s);
+      if (e != hipSuccess) return e;
+      hipLaunchKernelGGL((k_onesweep<kOsBlock, kOsIpt, true, false, 1, false, false, 1>), gd, bd, 0, s, in, out,
+                         m, shift, next_shift, sub_hist, next_hist, st, tile_ctr, epoch, err, nullptr, nullptr,
+                         SegPass(), gsrc, rp);
+    } else if (next_shift >= 0) {
+      hipLaunchKernelGGL((k_onesweep<kOsBlock, kOsIpt, true, false, 1, false, false, 2>), gd, bd, 0, s, in, out,
+                         m, shift, next_shift, sub_hist, next_hist, st, tile_ctr, epoch, err, nullptr, nullptr,
+                         SegPass(), gsrc, rp);
+    } else {
+      hipLaunchKernelGGL((k_onesweep<kOsBlock, kOsIpt, false, false, 1, false, false, 2>), gd, bd, 0, s, in, out,
+                         m, shift, 0, sub_hist, nullptr, st, tile_ctr, epoch, err, nullptr, nullptr, SegPass(),
+                         gsrc, rp);
+    }
+  } else if (extra.probe) {
     // The placement probe: a last pass, whole stage, under its own name.
     if (next_shift >= 0 || c16 || extra.halves != 1 || extra.seg || gat) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_onesweep_probe, gd, bd, 0, s, in, out, m, shift, 0, sub_hist, nullptr, st, tile_ctr,
@@ -2010,7 +2138,7 @@ hipError_t launch_onesweep(const Elem* in, Elem* out, int64_t m, int shift, int 
       return hipErrorInvalidValue;
     hipLaunchKernelGGL((k_onesweep<kOsBlock, kOsIpt, false, false, 1, true>), gd, bd, 0, s, in, out, m,
                        shift, 0, sub_hist, nullptr, st, tile_ctr, epoch, err, extra.totals, nullptr,
-                       *extra.seg, gsrc);
+                       *extra.seg, gsrc, RegionPass());
   } else if (c16) {
     // The 16-bit counts need the low byte below this digit, and no next
     // digit: the exchange follows this pass.

@@ -75,6 +75,12 @@ bool onesweep_applies(const lsb_ctx* c) {
          c->ranks[0].here <= lsb::kOnesweepMaxElems;
 }
 
+// The regional first pass's rg_buf words (region_sample, region_first): [kRgCounts, +2048) region counts, [kRgHist, +256) the
+// sample's digit counts, kRgOvf the overflow word, [kRgSpan, +4) the
+// sample's span (2 u64).
+constexpr int kRgCounts = 0, kRgHist = lsb::kRegions, kRgOvf = kRgHist + lsb::kBuckets,
+              kRgSpan = kRgOvf + 2, kRgWords = kRgSpan + 4;
+
 int onesweep_ensure(Rank& r) {
   if (r.os_status) return LSB_OK;
   const size_t tiles = (size_t)lsb::onesweep_tiles(r.here);
@@ -88,6 +94,14 @@ int onesweep_ensure(Rank& r) {
   HIP_TRY(hipMemsetAsync(r.os_ctr, 0, 2 * lsb::kOnesweepSubs * sizeof(uint32_t), r.stream));
   r.os_epoch = 0;
   r.os_grid = max_chunks_for_device(r.dev);
+  if (r.rg_cap > 0) {  // the regional first pass's buffers (region_ensure)
+    const size_t rows = (size_t)lsb::onesweep_tiles(r.rg_cap * lsb::kRegions) * lsb::kBuckets;
+    LSB_TRY(dev_alloc(&r.rg_buf, (size_t)kRgWords));
+    LSB_TRY(host_alloc(&r.rg_h, (size_t)kRgWords));
+    LSB_TRY(dev_alloc(&r.os_status2, rows));
+    HIP_TRY(hipMemsetAsync(r.os_status2, 0, rows * sizeof(uint32_t), r.stream));
+    r.os_epoch2 = 0;
+  }
   return LSB_OK;
 }
 
@@ -99,15 +113,32 @@ int onesweep_ensure(Rank& r) {
 // kernel runs writes no rows, and a later launch would then accept rows of
 // two launches back as current.  So a failure marks the rows dirty; the next
 // launch zeroes them first and restarts the epochs (the first is odd).
+// The pass that reads the regional layout (region_mode 2) has more tiles
+// than the others and keeps its rows on a track of its own (os_status2,
+// os_epoch2).
+void zero_status(Rank& r) {
+  (void)hipMemsetAsync(r.os_status, 0, (size_t)lsb::onesweep_tiles(r.here) * lsb::kBuckets * sizeof(uint32_t),
+                       r.stream);
+  if (r.os_status2)
+    (void)hipMemsetAsync(r.os_status2, 0,
+                         (size_t)lsb::onesweep_tiles(r.rg_cap * lsb::kRegions) * lsb::kBuckets * sizeof(uint32_t),
+                         r.stream);
+  r.os_epoch = 0;
+  r.os_epoch2 = 0;
+}
+
 int onesweep_launch(lsb_ctx* c, Rank& r, int shift, int next, const uint32_t* hist,
                     uint32_t* next_hist, lsb::OnesweepExtra x) {
-  const size_t status_bytes = (size_t)lsb::onesweep_tiles(r.here) * lsb::kBuckets * sizeof(uint32_t);
   if (r.os_dirty) {
-    HIP_TRY(hipMemsetAsync(r.os_status, 0, status_bytes, r.stream));
-    r.os_epoch = 0;
+    zero_status(r);
+    HIP_TRY(hipGetLastError());
     r.os_dirty = false;
   }
-  uint32_t epoch = r.os_epoch + 1;
+  const bool track2 = x.region_mode == 2;
+  uint32_t* status = track2 ? r.os_status2 : r.os_status;
+  uint32_t& last_epoch = track2 ? r.os_epoch2 : r.os_epoch;
+  if (!status) return fail(LSB_ERR_INVALID, "onesweep_launch", "regional layout's look-back rows");
+  uint32_t epoch = last_epoch + 1;
   if (epoch >= (1u << 30)) epoch = 2;  // 2^30 is even: keep the alternation
   hipError_t e;
   if (c->fail_onesweep > 0 && --c->fail_onesweep == 0) {  // LSB_OPT_FAIL_ONESWEEP (tests)
@@ -116,7 +147,7 @@ int onesweep_launch(lsb_ctx* c, Rank& r, int shift, int next, const uint32_t* hi
   }
   {
     Timer t(c, &r, LSB_K_SCATTER);
-    e = lsb::launch_onesweep(r.A, r.B, r.here, shift, next, hist, next_hist, r.os_status, r.os_ctr,
+    e = lsb::launch_onesweep(r.A, r.B, r.here, shift, next, hist, next_hist, status, r.os_ctr,
                              epoch, r.os_ctr + lsb::kOnesweepSubs, r.os_grid, r.stream, x);
   }
   if (e != hipSuccess) {
@@ -124,7 +155,7 @@ int onesweep_launch(lsb_ctx* c, Rank& r, int shift, int next, const uint32_t* hi
     r.os_dirty = true;
     return fail(LSB_ERR_HIP, "launch_onesweep", hipGetErrorString(e));
   }
-  r.os_epoch = epoch;
+  last_epoch = epoch;
   count_pass_elems(c, r.here);
   std::swap(r.A, r.B);
   return LSB_OK;
@@ -171,17 +202,94 @@ std::vector<int> varying_bytes(uint64_t varying) {
 // One k_onesweep pass per byte of `digits` (ascending), r.A -> r.B ->
 // ..., each also counting the next byte over its output; os_hist[0] holds
 // the sub-array histogram of digits[0] over r.A.
-int onesweep_digits(lsb_ctx* c, Rank& r, const std::vector<int>& digits, int* passes) {
+// From digits[from] on; rp: digits[from]'s pass reads the regional layout
+// (its input's histogram in os_hist[from & 1]).
+int onesweep_digits(lsb_ctx* c, Rank& r, const std::vector<int>& digits, int* passes, size_t from = 0,
+                    const lsb::RegionPass* rp = nullptr) {
   uint32_t* hist[2] = {r.os_hist, r.os_hist + lsb::kOnesweepSubs * lsb::kBuckets};
-  for (size_t i = 0; i < digits.size(); ++i) {
+  for (size_t i = from; i < digits.size(); ++i) {
     const int shift = digits[i] * lsb::kDigitBits;
     const int next = i + 1 < digits.size() ? digits[i + 1] * lsb::kDigitBits : -1;
     begin_pass(c, shift);
     lsb::OnesweepExtra x;
     x.halves = r.os_halves;
+    if (rp && i == from) {
+      x.region = rp;
+      x.region_mode = 2;
+    }
     LSB_TRY(onesweep_launch(c, r, shift, next, hist[i & 1], hist[(i + 1) & 1], x));
     ++*passes;
   }
+  return LSB_OK;
+}
+
+// ---- the regional first pass (LSB_OPT_REGION_FIRST) ------------
+// A P == 1 LSD sort's first pass takes no histogram read (k_subhist, 16 B per
+// record): k_onesweep writes digit 0's records into 2048 regions of slots
+// (digit b, sub-array x), each as long as a uniform region could need with
+// ample slack, so their offsets come from the look-back alone; the second
+// pass reads that layout region by region (its valid prefix per tile) and
+// writes the dense one.  The first pass also counts the regions and digit 1
+// over the layout's tiles.  A sample of 2^20 records decides beforehand:
+// every byte of the sampled keys must vary (then every digit varies, and no
+// key span is needed: all passes run) and no bucket of digit 0 may hold over
+// 1.1 / 256 of the sample; skewed or structured keys take the usual start,
+// k_subhist's read with the exact span.  A region that still overflows sets
+// a word the host reads after the first pass, and the sort then starts over
+// from the input, which the first pass left in place.
+
+bool region_applies(const lsb_ctx* c, const Rank& r) {
+  return c->region && !exchanging(c) && c->onesweep && c->os_split == 0 && c->hybrid == 0 && r.rg_cap > 0 &&
+         r.here == c->per && r.cap >= r.rg_cap * lsb::kRegions && r.here <= lsb::kOnesweepMaxElems;
+}
+
+lsb::RegionPass region_pass(Rank& r) {
+  lsb::RegionPass rp;
+  rp.cap = r.rg_cap;
+  rp.counts = r.rg_buf + kRgCounts;
+  rp.ovf = r.rg_buf + kRgOvf;
+  return rp;
+}
+
+// The sample (filed as the sort's count): *go = take the regional pass;
+// *seen = the key bits that vary in the sample.
+int region_sample(lsb_ctx* c, Rank& r, bool* go, uint64_t* seen) {
+  *go = false;
+  if (!r.os_status2) return LSB_OK;  // allocated by onesweep_ensure
+  {
+    Timer t(c, &r, LSB_K_UPSWEEP);
+    HIP_TRY(lsb::launch_sample(r.A, r.here, 0, r.rg_buf + kRgHist,
+                               reinterpret_cast<uint64_t*>(r.rg_buf + kRgSpan), r.stream));
+  }
+  HIP_TRY(hipMemcpyAsync(r.rg_h + kRgHist, r.rg_buf + kRgHist, (size_t)(kRgWords - kRgHist) * sizeof(uint32_t),
+                         hipMemcpyDeviceToHost, r.stream));
+  HIP_TRY(hipStreamSynchronize(r.stream));
+  uint64_t S = 0, top = 0;
+  for (int b = 0; b < lsb::kBuckets; ++b) {
+    S += r.rg_h[kRgHist + b];
+    top = std::max<uint64_t>(top, r.rg_h[kRgHist + b]);
+  }
+  uint64_t sp[2];
+  memcpy(sp, r.rg_h + kRgSpan, sizeof sp);
+  *seen = sp[0] & sp[1];
+  bool every_byte = true;
+  for (int b = 0; b < 64 / lsb::kDigitBits; ++b)
+    every_byte = every_byte && ((*seen >> (b * lsb::kDigitBits)) & (lsb::kBuckets - 1)) != 0;
+  *go = every_byte && top * lsb::kBuckets * 10 <= S * 11;
+  return LSB_OK;
+}
+
+// Pass 0 into the regional layout (r.A -> r.B, then they swap), counting
+// digit 1 into os_hist[1]; the overflow word's read-back is queued.
+int region_first(lsb_ctx* c, Rank& r, int* passes) {
+  const lsb::RegionPass rp = region_pass(r);
+  begin_pass(c, 0);
+  lsb::OnesweepExtra x;
+  x.region = &rp;
+  x.region_mode = 1;
+  LSB_TRY(onesweep_launch(c, r, 0, lsb::kDigitBits, nullptr, r.os_hist + lsb::kOnesweepSubs * lsb::kBuckets, x));
+  ++*passes;
+  HIP_TRY(hipMemcpyAsync(r.rg_h + kRgOvf, r.rg_buf + kRgOvf, sizeof(uint32_t), hipMemcpyDeviceToHost, r.stream));
   return LSB_OK;
 }
 
@@ -244,6 +352,7 @@ struct LocalSort {
   bool hist_queued = false;  // its read-back into os_hist_h is queued
   std::vector<int> digits, msd;
   bool fuse = false;
+  bool region = false;  // pass 0 ran into the regional layout (region_first)
   // {A, B, R} stays a permutation of {X0, X1, X2} at every step (the pass
   // loop swaps A and B; R holds X0, the kept input, from the first pass on).
   // While armed, an error return restores A = X0, B = X1, R = X2, so the
@@ -335,6 +444,13 @@ int LocalSort::begin() {
     hist_queued = true;
   } else {
     kind = kLsd;
+    region = false;
+    if (region_applies(c, r)) LSB_TRY(region_sample(c, r, &region, &varying));
+    if (region) {  // every digit varies: no span read
+      c->last_first = LSB_FIRST_REGIONAL;
+      return region_first(c, r, &passes);
+    }
+    varying = ~0ull;
     LSB_TRY(count_byte(c, r, 0, c->skip_constant));
     LSB_TRY(queue_halves(c, r, r.os_hist));
   }
@@ -376,10 +492,40 @@ int LocalSort::queue() {
   Step step(*this);
   HIP_TRY(hipSetDevice(r.dev));
   const int64_t m = r.here;
-  if (c->skip_constant) {
+  if (kind == kLsd && region) {
+    // Every digit varies (region_sample).  The second pass reads the
+    // regional layout (pass 0 counted digit 1 over its tiles into os_hist[1]).
+    region = false;
     HIP_TRY(hipStreamSynchronize(r.stream));
-    varying = r.span_h[0] & r.span_h[1];
+    digits = varying_bytes(~0ull);
+    if (r.rg_h[kRgOvf] == 0) {
+      r.os_halves = 1;
+      const lsb::RegionPass rp = region_pass(r);
+      LSB_TRY(onesweep_digits(c, r, digits, &passes, 1, &rp));
+      kind = kDone;
+      return queue_err_word();
+    }
+    // A region overflowed: start over from the input, kept in place (pass 0
+    // read it and wrote the other buffer), with the usual first read.
+    c->last_first = LSB_FIRST_REGIONAL_REDONE;
+    std::swap(r.A, r.B);
+    passes = 0;
+    c->pass_cursor = 0;
+    c->cur_pass = 0;
+    HIP_TRY(hipMemsetAsync(r.span, 0, 2 * sizeof(uint64_t), r.stream));
+    LSB_TRY(count_byte(c, r, 0, c->skip_constant));
+    LSB_TRY(queue_halves(c, r, r.os_hist));
+    HIP_TRY(hipMemcpyAsync(r.span_h, r.span, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, r.stream));
+    HIP_TRY(hipStreamSynchronize(r.stream));
+    varying = c->skip_constant ? r.span_h[0] & r.span_h[1] : ~0ull;
+    digits = varying_bytes(varying);
+    LSB_TRY(choose_halves(c, r, true));
+    LSB_TRY(onesweep_digits(c, r, digits, &passes));
+    kind = kDone;
+    return queue_err_word();
   }
+  if (c->skip_constant) HIP_TRY(hipStreamSynchronize(r.stream));
+  if (c->skip_constant) varying = r.span_h[0] & r.span_h[1];
   digits = varying_bytes(varying);
   if (kind == kLsd) {
     if (!digits.empty() && digits[0] != 0) {
@@ -568,8 +714,8 @@ int onesweep_check(Rank& r) {
   HIP_TRY(hipMemset(r.os_ctr + lsb::kOnesweepSubs, 0, sizeof(uint32_t)));
   // A launch that gave up may have left rows of an older parity: start the
   // granules over (zeroed; the next launch is odd).
-  HIP_TRY(hipMemset(r.os_status, 0, (size_t)lsb::onesweep_tiles(r.here) * lsb::kBuckets * sizeof(uint32_t)));
-  r.os_epoch = 0;
+  zero_status(r);
+  HIP_TRY(hipStreamSynchronize(r.stream));
   return fail(LSB_ERR_HIP, "k_onesweep", "look-back timed out; output invalid");
 }
 

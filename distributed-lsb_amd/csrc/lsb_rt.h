@@ -93,6 +93,18 @@ struct Rank {
   bool os_dirty = false;                // a launch failed: zero os_status before the next
   int64_t* seg_base = nullptr;          // [kOnesweepSubs][256] the hybrid's bucket bases (k_segfix)
   int os_grid = 0;                      // persistent grid (2 workgroups per CU)
+  // The regional first pass (LSB_OPT_REGION_FIRST), allocated on first use:
+  // the look-back rows of the pass that reads the regional layout (a track
+  // of their own: that pass has more tiles than the others, and a status
+  // buffer must only ever see one tile count), its epoch,
+  // and rg_buf: region counts, the sample's histogram and span, the overflow
+  // word (kRg* offsets, lsb_passes.cpp), rg_h its pinned mirror.
+  int64_t cap = 0;                      // records A and B hold (>= here)
+  int64_t rg_cap = 0;                   // slots per region (0: no regional first pass)
+  uint32_t* os_status2 = nullptr;
+  uint32_t os_epoch2 = 0;
+  uint32_t* rg_buf = nullptr;
+  uint32_t* rg_h = nullptr;
   // Per-digit exchange with single-read local passes (sort_exchange_onesweep):
   // os_hist[os_cur] is A's sub-array histogram of the byte at os_valid (-1:
   // none; the next pass reads A once with k_subhist).  The exchange's
@@ -148,6 +160,7 @@ struct lsb_ctx {
   bool peer = false;          // exchange by direct stores into the owners' buffers
   bool peer_ready = false;    // peer tables set up
   bool onesweep = true;       // P == 1: single-read passes (k_subhist + k_onesweep)
+  bool region = true;         // LSB_OPT_REGION_FIRST: P == 1 LSD sorts start with the regional pass
   bool self_coll = false;     // the self segment also goes through the collective
   bool gather = true;         // LSB_OPT_EXCHANGE_GATHER: count-only placement + gathered pass
   int os_split = 0;           // LSB_OPT_ONESWEEP_SPLIT: 0 auto, 1 never, 2 always
@@ -159,6 +172,7 @@ struct lsb_ctx {
   int last_local_passes = 0;
   int last_exchanges = 0;
   uint64_t last_varying = 0;
+  int last_first = 0;  // the first pass's form (lsb_get_first_pass)
   lsb::KeyGen keygen;
   std::vector<lsb_rt::PendingEvent> pending;
   std::vector<std::pair<int, hipEvent_t>> event_pool;  // (device, event) of finished timings
@@ -276,6 +290,12 @@ size_t rec_bytes(size_t count);  // device bytes rec_alloc takes for count recor
 void rec_free(void* p);
 bool rec_is_vmm(const void* p);
 int max_chunks_for_device(int dev);
+// Records A and B are allocated for: the block, or the regional first
+// pass's slots when a P == 1 context's sorts may start with it (blocks of at
+// least region_min() records: lsb::kRegionMin, or LSB_REGION_MIN >= 2^16).
+int64_t region_min();
+int64_t region_cap_for(int64_t per, int P);
+int64_t record_capacity(int64_t per, int P);
 int alloc_records(lsb_ctx* c, Rank& r);  // A and B (placement-calibrated)
 int alloc_third(lsb_ctx* c, Rank& r);    // R, placed against A and B
 int init_rank(lsb_ctx* c, Rank& r, int rank, int dev);

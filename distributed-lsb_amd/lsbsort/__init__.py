@@ -54,6 +54,8 @@ OPT_ONESWEEP_SPLIT = 8
 OPT_HYBRID = 9
 OPT_EXCHANGE_GATHER = 10
 OPT_FAIL_ONESWEEP = 11
+OPT_REGION_FIRST = 12
+FIRST_COUNT, FIRST_REGIONAL, FIRST_REGIONAL_REDONE = 0, 1, 2
 MAX_PASSES = 16
 
 
@@ -156,6 +158,7 @@ def _lib() -> ctypes.CDLL:
             "lsb_destroy": (None, [vp]),
             "lsb_set_option": (i32, [vp, i32, i64]),
             "lsb_get_last_sort": (i32, [vp, vp, vp, vp]),
+            "lsb_get_first_pass": (i32, [vp, vp]),
             "lsb_local_ranks": (i32, [vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
             "lsb_generate": (i32, [vp]),
             "lsb_generate_ex": (i32, [vp, i32, ctypes.c_double]),
@@ -482,6 +485,13 @@ class World:
         _check(_lib().lsb_get_last_sort(self._h, ctypes.byref(lp), ctypes.byref(ex), ctypes.byref(vb)),
                "lsb_get_last_sort")
         return int(lp.value), int(ex.value), int(vb.value)
+
+    def first_pass(self) -> int:
+        """How the last my_sort began (lsb_get_first_pass): FIRST_COUNT,
+        FIRST_REGIONAL or FIRST_REGIONAL_REDONE."""
+        f = ctypes.c_int()
+        _check(_lib().lsb_get_first_pass(self._h, ctypes.byref(f)), "lsb_get_first_pass")
+        return int(f.value)
 
     def kernel_stats(self) -> dict:
         out = {}

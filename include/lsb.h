@@ -136,6 +136,17 @@ typedef struct lsb_ctx lsb_ctx_t;
                                       as a failed launch would; 0 (default) off.  The context
                                       stays usable: its buffers keep their roles and the next
                                       sort starts from the input still in A. */
+#define LSB_OPT_REGION_FIRST    12 /* P == 1 sorts of >= 2^27 records by the LSD passes:
+                                      1 (default) the first pass takes no histogram read: it
+                                      writes each (digit, sub-array) class of records into a
+                                      slot range of its own, sized with slack over a uniform
+                                      class (A and B hold 2.3 % more slots at 2^30), and the
+                                      second pass reads that layout back to a dense one.  A
+                                      2^20-record sample sends skewed or structured low bytes
+                                      to the usual start (a histogram read), and a range that
+                                      overflows all the same makes the sort start over from
+                                      its input.  0: every sort starts with the histogram
+                                      read.  Same output. */
 
 /* ---- geometry: DistributedArray::create (mpi/mpi_lsbsort.cpp:144-149) ---- */
 int64_t lsb_per_rank(int64_t n_total, int num_ranks);            /* ceil(n/P) */
@@ -230,6 +241,17 @@ int  lsb_sort(lsb_ctx_t* ctx);
  * and not forced) and the key bits that vary (~0 when skipping is off). */
 int  lsb_get_last_sort(lsb_ctx_t* ctx, int* local_passes, int* exchanges,
                        uint64_t* varying_bits);
+/* How the last lsb_sort began (LSB_OPT_REGION_FIRST): LSB_FIRST_COUNT a
+ * histogram read (k_subhist / k_upsweep) before the first pass, or none ran;
+ * LSB_FIRST_REGIONAL the regional first pass; LSB_FIRST_REGIONAL_REDONE the
+ * regional pass overflowed a region, and the sort started over from its
+ * input with the histogram read.  With LSB_FIRST_REGIONAL the varying bits
+ * of lsb_get_last_sort are those of a 2^20-record sample (every byte varies
+ * there, so every pass runs). */
+#define LSB_FIRST_COUNT           0
+#define LSB_FIRST_REGIONAL        1
+#define LSB_FIRST_REGIONAL_REDONE 2
+int  lsb_get_first_pass(lsb_ctx_t* ctx, int* form);
 /* == globalShuffle(A, B, digit): one pass, result in A. */
 int  lsb_pass(lsb_ctx_t* ctx, int digit);
 int  lsb_sync(lsb_ctx_t* ctx);

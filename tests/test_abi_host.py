@@ -349,8 +349,16 @@ def test_rank_footprint_model(lsb_built, monkeypatch):
     monkeypatch.delenv("LSB_PLACEMENT_CANDIDATES", raising=False)
     monkeypatch.delenv("LSB_RECORD_ALLOC", raising=False)
     monkeypatch.delenv("LSB_VMM_CHUNK_MIB", raising=False)
+    monkeypatch.delenv("LSB_REGION_MIN", raising=False)
     n = 1 << 30
     rows = (n // 4096) * 256 * 4
+    # P == 1 blocks of >= 2^27 records: A and B hold the regional first pass's
+    # slots (2048 regions of 131 tiles at 2^30: 17 pieces each) and its pass
+    # over them has look-back rows of its own.
+    slots = 2048 * 131 * 4096
+    f = L.rank_footprint(n, 1, 8)
+    assert 0 <= f["bytes"] - 34 * gib - rows - (slots // 4096) * 256 * 4 < 64 << 20
+    monkeypatch.setenv("LSB_REGION_MIN", str(1 << 40))  # no regional slots from here on
     f = L.rank_footprint(n, 1, 8)
     assert f["probe_bytes"] == 0 and 0 <= f["bytes"] - 32 * gib - rows < 64 << 20
     extra = L.rank_footprint(n, 1, 8, with_recv=True)["bytes"] - f["bytes"]
