@@ -294,6 +294,9 @@ lsb_ctx* new_ctx(int64_t n_total, int num_ranks, int radix_bits) {
   c->per = div_ceil(n_total, num_ranks);
   c->bits = radix_bits;
   c->nb = radix_bits == 64 ? lsb::kBuckets : 1 << radix_bits;
+  // LSB_REGION_FIRST=0: contexts start with the option off (A/B runs of
+  // programs that do not set options, e.g. bench.py).
+  if (const char* e = getenv("LSB_REGION_FIRST")) c->region = atoi(e) != 0;
   return c;
 }
 
