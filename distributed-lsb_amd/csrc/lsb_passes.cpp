@@ -10,6 +10,8 @@
 //     bytes, segments ordered by k_segfix / k_segsort (lsb_segsort.hip).
 #include "lsb_rt.h"
 
+#include <cmath>
+
 #include <deque>
 
 namespace lsb_rt {
@@ -233,7 +235,8 @@ int onesweep_digits(lsb_ctx* c, Rank& r, const std::vector<int>& digits, int* pa
 // over the layout's tiles.  A sample of 2^20 records decides beforehand:
 // every byte of the sampled keys must vary (then every digit varies, and no
 // key span is needed: all passes run) and no bucket of digit 0 may hold over
-// 1.1 / 256 of the sample; skewed or structured keys take the usual start,
+// 1.1 / 256 of the sample (6 standard deviations over the mean in small
+// samples); skewed or structured keys take the usual start,
 // k_subhist's read with the exact span.  A region that still overflows sets
 // a word the host reads after the first pass, and the sort then starts over
 // from the input, which the first pass left in place.
@@ -275,7 +278,10 @@ int region_sample(lsb_ctx* c, Rank& r, bool* go, uint64_t* seen) {
   bool every_byte = true;
   for (int b = 0; b < 64 / lsb::kDigitBits; ++b)
     every_byte = every_byte && ((*seen >> (b * lsb::kDigitBits)) & (lsb::kBuckets - 1)) != 0;
-  *go = every_byte && top * lsb::kBuckets * 10 <= S * 11;
+  // No bucket over the mean by more than max(10 %, 6 standard deviations of
+  // a uniform bucket's count in a sample this size).
+  const double mean = (double)S / lsb::kBuckets;
+  *go = every_byte && S > 0 && (double)top <= mean + std::max(0.1 * mean, 6.0 * std::sqrt(mean));
   return LSB_OK;
 }
 
