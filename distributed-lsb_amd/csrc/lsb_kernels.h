@@ -189,16 +189,24 @@ constexpr int64_t kRegionMin = int64_t(1) << 27;
 constexpr int kRegions = kBuckets * kOnesweepSubs;  // 2048
 inline int64_t region_mean(int64_t m) { return (m + kRegions - 1) / kRegions; }
 // Slots per region for m records (0: fewer than min_m records, too few for
-// the form): the mean plus max(mean / 64, 16 standard deviations of a
-// uniform region's count), rounded up to whole tiles.  2^27 records: +6.25 %
-// slots; 2^30: +2.3 %.  (Tests lower min_m to cover small sorts, whose
-// regions are then one mostly empty tile each.)
+// the form): the mean plus max(mean / 64, 6 standard deviations of a uniform
+// region's count), rounded up to whole tiles.  2^27 records: +6.25 % slots;
+// 2^30: +1.6 % (130 tiles per region).  (Tests lower min_m to cover small
+// sorts, whose regions are then one mostly empty tile each.)  The two
+// constants are build knobs for experiments (tools/r05/region_slack.sh).
+#ifndef LSB_REGION_SIGMA
+#define LSB_REGION_SIGMA 6
+#endif
+#ifndef LSB_REGION_DIV
+#define LSB_REGION_DIV 64
+#endif
 inline int64_t region_cap(int64_t m, int64_t min_m = kRegionMin) {
   if (m < min_m || m <= 0) return 0;
   const int64_t mu = region_mean(m);
   int64_t sd = 1;
   while (sd * sd < mu) ++sd;
-  const int64_t slack = mu / 64 > 16 * sd ? mu / 64 : 16 * sd;
+  const int64_t a = mu / LSB_REGION_DIV, b = LSB_REGION_SIGMA * sd;
+  const int64_t slack = a > b ? a : b;
   return (mu + slack + kTile - 1) / kTile * kTile;
 }
 inline int64_t region_slots(int64_t m, int64_t min_m = kRegionMin) { return region_cap(m, min_m) * kRegions; }

@@ -140,7 +140,7 @@ typedef struct lsb_ctx lsb_ctx_t;
                                       1 (default) the first pass takes no histogram read: it
                                       writes each (digit, sub-array) class of records into a
                                       slot range of its own, sized with slack over a uniform
-                                      class (A and B hold 2.3 % more slots at 2^30), and the
+                                      class (A and B hold 1.6 % more slots at 2^30), and the
                                       second pass reads that layout back to a dense one.  A
                                       2^20-record sample sends skewed or structured low bytes
                                       to the usual start (a histogram read), and a range that

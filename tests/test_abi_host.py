@@ -353,9 +353,9 @@ def test_rank_footprint_model(lsb_built, monkeypatch):
     n = 1 << 30
     rows = (n // 4096) * 256 * 4
     # P == 1 blocks of >= 2^27 records: A and B hold the regional first pass's
-    # slots (2048 regions of 131 tiles at 2^30: 17 pieces each) and its pass
+    # slots (2048 regions of 130 tiles at 2^30: 17 pieces each) and its pass
     # over them has look-back rows of its own.
-    slots = 2048 * 131 * 4096
+    slots = 2048 * 130 * 4096
     f = L.rank_footprint(n, 1, 8)
     assert 0 <= f["bytes"] - 34 * gib - rows - (slots // 4096) * 256 * 4 < 64 << 20
     monkeypatch.setenv("LSB_REGION_MIN", str(1 << 40))  # no regional slots from here on
