@@ -55,6 +55,7 @@ METRIC = "Melem/s (16-byte elems) at 1/2/4/8 GPUs; per-pass HBM GB/s vs roofline
 HBM_PEAK_GBS = 8000.0           # MI355X HBM3E spec (MI355X_MICROARCH.md)
 SCATTER_BYTES_PER_ELEM = 32     # 16 B read + 16 B written per record per pass
 COUNT_BYTES_PER_ELEM = 16       # histogram read of the keys' lines
+SAMPLE_RECORDS = 1 << 20        # the regional first pass's sample (256 tiles of 4096 records)
 REF_MPI_MELEMS = 830.0          # mpi_lsbsort, 64 nodes x 128 cores, n = 2^36
 XGMI_LINK_GBS = 153.0           # per xGMI link of an MI355X (spec figure, see XGMI_PEAK_SOURCE)
 XGMI_PEAK_SOURCE = ("spec figure, not measured here: MI355X, 7 xGMI links x ~153 GB/s per GPU, one direct link "
@@ -882,6 +883,7 @@ def main():
     xstats = w.exchange_stats()
     placement = w.placement()
     last = w.last_sort()
+    first = w.first_pass()  # the regional first pass (no count read) or a count read
     w.close()
     mem = memory_keys(a, N, radix, lsbsort.device_memory(device)[1],
                       max(1, N // max(1, visible_devices())) if N > 1 else 1)
@@ -932,8 +934,11 @@ def main():
                 "avg_launch_ms": round(scatter_ms / launches, 4)}
     # Algorithmic bytes of a sort: 32 B per record per scatter launch, 16 B
     # per count read (one per pass for reduce-then-scan, one per sort for
-    # single-read passes).
-    per_elem = (SCATTER_BYTES_PER_ELEM * launches + COUNT_BYTES_PER_ELEM * stats["upsweep"][0]) / a.steps
+    # single-read passes; none when the sort starts with the regional first
+    # pass, whose count launch is a sample of 2^20 records).
+    count_elem = (COUNT_BYTES_PER_ELEM * min(1.0, SAMPLE_RECORDS / max(1, n_total / N))
+                  if first == lsbsort.FIRST_REGIONAL else COUNT_BYTES_PER_ELEM)
+    per_elem = (SCATTER_BYTES_PER_ELEM * launches + count_elem * stats["upsweep"][0]) / a.steps
     sort_gbs = per_elem * (n_total / N) / (ms_per_step / 1e3) / 1e9
     # SURVEY.md §8(d)'s sort-level figure: 48 B per record per digit pass
     # (16 B histogram read + 32 B scatter) over D = 64 / radix_bits passes,
@@ -960,10 +965,14 @@ def main():
                    "local_digit_bits": 8, "local_passes": last[0], "exchanges": last[1],
                    "pass_form": ("hybrid (k_subhist, k_onesweep on the top varying bytes, then one "
                                  "k_segsort of the runs equal on them)" if a.passes == "hybrid" else
-                                 ("single-read (k_subhist once, k_onesweep per pass" +
+                                 ("single-read (" + ("a 2^20-record sample, then the regional first pass "
+                                                     "(no count read; DESIGN.md 4), k_onesweep per pass"
+                                                     if first == lsbsort.FIRST_REGIONAL else
+                                                     "k_subhist once, k_onesweep per pass") +
                                   ("; k_place counts the next pass's histogram)" if N > 1 and radix != 64
                                    else ")")) if kernel == "k_onesweep"
                                  else "reduce-then-scan (k_upsweep, k_scan, k_scatter per pass)"),
+                   "first_pass": {0: "count read", 1: "regional", 2: "regional, overflowed: redone"}.get(first),
                    "exchange_digit_bits": radix if N > 1 else None,
                    "record_bytes": 16, "dist": a.dist,
                    "parallelism": parallelism(N, radix, a)},
@@ -977,7 +986,8 @@ def main():
         "kernel_ms_per_step": {k: round(v[1] / a.steps, 3) for k, v in stats.items()},
         "per_pass": per_pass_rows(passes, a.steps, kernel, N),
         "kernel_ms_per_step_legend": {
-            "upsweep": "count read (k_subhist once per sort, or k_upsweep per pass)",
+            "upsweep": "count read (k_subhist once per sort, or k_upsweep per pass; with the regional "
+                       "first pass: the 2^20-record sample)",
             "scan": "chunk scan (k_scan, reduce-then-scan only)",
             "scatter": "local passes (k_onesweep, or k_scatter)",
             "exchange": "exchange on the rank's stream: splitter search + all-to-all (whole key) "
