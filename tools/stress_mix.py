@@ -10,7 +10,12 @@ thinned out at random -- constant bytes, few distinct values in the middle
 bytes, duplicates -- the inputs that take the hybrid's fallbacks and
 k_segfix's long crossing runs; those are checked against numpy's stable
 argsort.  Record buffers come from VMM pieces of a drawn size (2 MiB,
-64 MiB or the default 1 GiB), so small sorts run the VMM allocator too.  Runs until --seconds have passed; one line per iteration.
+64 MiB or the default 1 GiB), so small sorts run the VMM allocator too.  The
+regional first pass (LSB_OPT_REGION_FIRST) starts at a drawn size (2^16
+records or the default 2^27), and some host-made keys crowd one digit-0
+bucket of one sub-array (the regions the sample may miss, so some sorts
+overflow one and start over); each line names how the sort began.  Runs
+until --seconds have passed; one line per iteration.
 
     python tools/stress_mix.py --seconds 240 --seed 1
 """
@@ -49,6 +54,21 @@ def thinned_keys(rng, n):
     return a
 
 
+def crowded_keys(rng, n):
+    """Uniform keys, except that a random share (up to 1/4) of one sub-array's
+    records get one digit-0 value: a region of the regional first pass that
+    can overflow where the sample does not look."""
+    g = np.random.default_rng(rng.randrange(1 << 30))
+    a = np.zeros(n, dtype=DT)
+    a["key"] = g.integers(0, 2**64 - 1, n, dtype=np.uint64)
+    a["val"] = np.arange(n, dtype=np.uint64)
+    x = rng.randrange(8)
+    lo, hi = x * n // 8, (x + 1) * n // 8
+    pick = lo + np.flatnonzero(g.random(hi - lo) < rng.uniform(0, 0.25))
+    a["key"][pick] = (a["key"][pick] & ~np.uint64(0xFF)) | np.uint64(rng.randrange(256))
+    return a
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=240)
@@ -69,13 +89,15 @@ def main():
         host = rng.random() < 1 / 3
         if host:
             n = min(n, 1 << 22)
-            dist = "thinned"
+            dist = "crowded" if rng.random() < 0.25 else "thinned"
+        region_min = rng.choice((1 << 16, 1 << 27))
+        os.environ["LSB_REGION_MIN"] = str(region_min)
         # record buffers from VMM pieces of 2 / 64 MiB (several pieces per
         # buffer at these sizes), or the default 1 GiB (hipMalloc below it)
         vmm = rng.choice((2, 64, 1024, 1024))
         os.environ["LSB_VMM_CHUNK_MIB"] = str(vmm)
         desc = (f"iter {it}: n={n} P={P} bits={bits} dist={dist} split={split} hybrid={hybrid} "
-                f"gather={gather} vmm={vmm}")
+                f"gather={gather} vmm={vmm} region_min={region_min}")
         t0 = time.time()
         try:
             with lsbsort.World(n, ranks=P, radix_bits=bits) as w:
@@ -83,7 +105,7 @@ def main():
                 w.set_option(lsbsort.OPT_HYBRID, hybrid)
                 w.set_option(lsbsort.OPT_EXCHANGE_GATHER, gather)
                 if host:
-                    arr = thinned_keys(rng, n)
+                    arr = crowded_keys(rng, n) if dist == "crowded" else thinned_keys(rng, n)
                     w.scatter_global(arr)
                     w.my_sort()
                     got = w.gather_global()
@@ -95,11 +117,13 @@ def main():
                     w.my_sort()
                     ok, first = w.verify()
                 srt = w.check_sorted()
+                form = w.first_pass()
         except lsbsort.LsbError as e:
-            ok, first, srt = False, str(e), False
+            ok, first, srt, form = False, str(e), False, -1
         if not (ok and srt):
             bad += 1
-        print(f"{desc} verify={ok} first_bad={first} sorted={srt} ms={(time.time() - t0) * 1e3:.0f}", flush=True)
+        print(f"{desc} first_pass={form} verify={ok} first_bad={first} sorted={srt} "
+              f"ms={(time.time() - t0) * 1e3:.0f}", flush=True)
         it += 1
     print(f"done: {bad} of {it} sorts wrong", flush=True)
     sys.exit(1 if bad else 0)
