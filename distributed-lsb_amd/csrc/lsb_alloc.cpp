@@ -291,7 +291,10 @@ int64_t region_min() {
 
 int64_t region_cap_for(int64_t per, int P) { return P == 1 ? lsb::region_cap(per, region_min()) : 0; }
 
-int64_t record_capacity(int64_t per, int P) { return std::max(per, region_cap_for(per, P) * lsb::kRegions); }
+int64_t record_capacity(int64_t per, int P) {
+  const int64_t cap = region_cap_for(per, P);
+  return cap > 0 ? std::max(per, lsb::region_stride(cap) * lsb::kRegions) : per;
+}
 
 int alloc_records(lsb_ctx* c, Rank& r) {
   const size_t per = (size_t)record_capacity(c->per, c->P);

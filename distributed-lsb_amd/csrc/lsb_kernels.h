@@ -209,7 +209,20 @@ inline int64_t region_cap(int64_t m, int64_t min_m = kRegionMin) {
   const int64_t slack = a > b ? a : b;
   return (mu + slack + kTile - 1) / kTile * kTile;
 }
-inline int64_t region_slots(int64_t m, int64_t min_m = kRegionMin) { return region_cap(m, min_m) * kRegions; }
+// Region r's first slot.  LSB_REGION_STAGGER (experiment): regions one tile
+// apart more than `cap`, each shifted by (37 r mod 16) x 256 records, so that
+// the first pass's 2048 write frontiers do not sit at one stride.
+#ifndef LSB_REGION_STAGGER
+#define LSB_REGION_STAGGER 0
+#endif
+__host__ __device__ inline int64_t region_stride(int64_t cap) { return cap + (LSB_REGION_STAGGER ? kTile : 0); }
+__host__ __device__ inline int64_t region_base(int64_t r, int64_t cap) {
+  return r * region_stride(cap) + (LSB_REGION_STAGGER ? ((r * 37) & 15) * 256 : 0);
+}
+// Records a buffer holding the regional layout needs.
+inline int64_t region_slots(int64_t m, int64_t min_m = kRegionMin) {
+  return region_stride(region_cap(m, min_m)) * kRegions;
+}
 struct RegionPass {
   int64_t cap = 0;                    // slots per region
   uint32_t* counts = nullptr;         // [kRegions] records per region

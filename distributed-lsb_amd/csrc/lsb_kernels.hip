@@ -866,6 +866,7 @@ __device__ __forceinline__ void onesweep_body(
   __shared__ uint64_t scan64[W];
   __shared__ uint32_t scan32[W];
   __shared__ int32_t s_tile, s_sub, s_nv;
+  __shared__ int64_t s_tb;
   __shared__ uint32_t tile_lo[2];  // C16: low byte of the tile's first, last record
   __shared__ TileDesc s_desc;      // GATHER: where this tile's records are
 
@@ -875,10 +876,9 @@ __device__ __forceinline__ void onesweep_body(
   const uint32_t lane = lane_id();
   // Tiles of this pass's input (TT) and of the next pass's (TTn: its
   // sub-arrays are what the next digit is counted by); output slots (mcap).
-  const int64_t slots = RG != 0 ? rg.cap * kRegions : m;
-  const int64_t TT = RG == 2 ? slots / T : (m + T - 1) / T;
-  const int64_t TTn = RG == 1 ? slots / T : (m + T - 1) / T;
-  const int64_t mcap = RG == 1 ? slots : m;
+  const int64_t TT = RG == 2 ? rg.cap / T * kRegions : (m + T - 1) / T;
+  const int64_t TTn = RG == 1 ? rg.cap / T * kRegions : (m + T - 1) / T;
+  const int64_t mcap = RG == 1 ? region_stride(rg.cap) * kRegions : m;
   uint32_t racc = 0;                     // RG = 1: thread t's count of region (t, cur_sub)
   // Granule tags (bits 30-31): this launch's parity, and the prefix bit.
   constexpr uint32_t kValMask = kStatusValMask, kPreBit = 1u << 30;
@@ -957,11 +957,14 @@ __device__ __forceinline__ void onesweep_body(
   // r holds that region's slots [k * T, (k + 1) * T)) while this tile is
   // written, so the loads at the loop top wait on nothing new.
   int nxt_nv = 0;
+  int64_t nxt_tb = 0;  // RG = 2: the tile's first slot
   auto region_nvalid = [&](int tl) -> int {
     if (tl < 0) return 0;
     const uint32_t ct = (uint32_t)(rg.cap / T);
     const uint32_t reg = (uint32_t)tl / ct;
-    const int64_t v = (int64_t)rg.counts[reg] - (int64_t)((uint32_t)tl - reg * ct) * T;
+    const uint32_t k = (uint32_t)tl - reg * ct;
+    nxt_tb = region_base(reg, rg.cap) + (int64_t)k * T;
+    const int64_t v = (int64_t)rg.counts[reg] - (int64_t)k * T;
     return (int)(v < 0 ? 0 : (v < T ? v : T));
   };
   if (t == 0) {
@@ -982,7 +985,10 @@ __device__ __forceinline__ void onesweep_body(
     if (t == 0) {
       s_tile = nxt_tile;
       s_sub = nxt_sub;
-      if (RG == 2) s_nv = nxt_nv;
+      if (RG == 2) {
+        s_nv = nxt_nv;
+        s_tb = nxt_tb;
+      }
     }
     if (GATHER && w == 0 && lane < 4) reinterpret_cast<uint4*>(&s_desc)[lane] = dreg;
 #pragma unroll
@@ -996,7 +1002,7 @@ __device__ __forceinline__ void onesweep_body(
       if (RG == 1) {
         if (bkt && cur_sub >= 0 && racc) atomicAdd(&rg.counts[t * kSub + cur_sub], racc);
         racc = 0;
-        base = (uint64_t)((bkt ? t : 0) * kSub + x) * (uint64_t)rg.cap;  // region (t, x)
+        base = (uint64_t)region_base((bkt ? t : 0) * kSub + x, rg.cap);  // region (t, x)
       } else {
         uint64_t pre = 0;
 #pragma unroll
@@ -1006,7 +1012,7 @@ __device__ __forceinline__ void onesweep_body(
       }
       cur_sub = x;
     }
-    const int64_t tb = (int64_t)tile * T;
+    const int64_t tb = RG == 2 ? s_tb : (int64_t)tile * T;
     const int nvalid = RG == 2 ? s_nv : (int)((m - tb) < T ? (m - tb) : T);
 
     Elem e[IPT];
@@ -1228,7 +1234,11 @@ __device__ __forceinline__ void onesweep_body(
       // stage position jb on (x1) when it crosses a sub-array boundary (at
       // most one: a non-empty sub-array holds >= kTile records).
       uint32_t c = 0xFFFFu;  // jb = 0xFFFF: never
-      if (cnt > 0) {
+      if (RG == 1) {
+        // Region (t, x) lies in the next pass's sub-array t / 32 (its
+        // sub-arrays are 256 whole regions): no run crosses one.
+        c = 0xFFFFu | ((uint32_t)(t >> 5) << 16) | ((uint32_t)(t >> 5) << 24);
+      } else if (cnt > 0) {
         const int x0 = sub_of_tile(R / T, TTn);
         const int64_t bnd = x0 + 1 < kSub ? sub_first_tile(x0 + 1, TTn) * T : mcap;
         if (R + cnt > bnd) {
@@ -2079,7 +2089,7 @@ hipError_t launch_onesweep(const Elem* in, Elem* out, int64_t m, int shift, int 
                                        rp.cap * kRegions < m || !rp.counts)))
     return hipErrorInvalidValue;
   // Tiles of the input: the regional layout's slots for its reading pass.
-  const int64_t TT = rm == 2 ? rp.cap * kRegions / kTile : (m + kTile - 1) / kTile;
+  const int64_t TT = rm == 2 ? rp.cap / kTile * kRegions : (m + kTile - 1) / kTile;
   auto* c16 = reinterpret_cast<unsigned long long*>(extra.count16);
   const bool gat = extra.gather != nullptr;
   // The split stage only for the plain and next-digit forms, never gathered

@@ -243,7 +243,8 @@ int onesweep_digits(lsb_ctx* c, Rank& r, const std::vector<int>& digits, int* pa
 
 bool region_applies(const lsb_ctx* c, const Rank& r) {
   return c->region && !exchanging(c) && c->onesweep && c->os_split == 0 && c->hybrid == 0 && r.rg_cap > 0 &&
-         r.here == c->per && r.cap >= r.rg_cap * lsb::kRegions && r.here <= lsb::kOnesweepMaxElems;
+         r.here == c->per && r.cap >= lsb::region_stride(r.rg_cap) * lsb::kRegions &&
+         r.here <= lsb::kOnesweepMaxElems;
 }
 
 lsb::RegionPass region_pass(Rank& r) {
