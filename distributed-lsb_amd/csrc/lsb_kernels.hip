@@ -953,23 +953,17 @@ __device__ __forceinline__ void onesweep_body(
   // The next tile's id is fetched while this tile's records are written
   // (a device-scope atomic is ~1 us under load; 3 % of the sort, measured).
   int nxt_tile = -1, nxt_sub = 0;
-  // RG = 2: thread 0 also reads the next tile's valid count (tile k of region
-  // r holds that region's slots [k * T, (k + 1) * T)) while this tile is
-  // written, so the loads at the loop top wait on nothing new.
-  int nxt_nv = 0;
-  int64_t nxt_tb = 0;  // RG = 2: the tile's first slot
-  auto region_nvalid = [&](int tl) -> int {
-    if (tl < 0) return 0;
-    const uint32_t ct = (uint32_t)(rg.cap / T);
-    const uint32_t reg = (uint32_t)tl / ct;
-    const uint32_t k = (uint32_t)tl - reg * ct;
-    nxt_tb = region_base(reg, rg.cap) + (int64_t)k * T;
-    const int64_t v = (int64_t)rg.counts[reg] - (int64_t)k * T;
-    return (int)(v < 0 ? 0 : (v < T ? v : T));
-  };
+  // RG = 2: thread 0 also reads the next tile's region count (tile k of
+  // region r holds that region's slots [k * T, (k + 1) * T)) while this tile
+  // is written, so the loads at the loop top wait on nothing new.
+  // The count is only consumed at the loop top, so the load's latency hides
+  // behind this tile's write-out (computing the valid count right away made
+  // wave 0, and with it the workgroup's closing barrier, wait for it).
+  uint32_t nxt_cnt = 0;  // RG = 2: the next tile's region count (its slots: region_slot)
+  auto region_next = [&](int tl) { nxt_cnt = tl < 0 ? 0u : rg.counts[(uint32_t)tl / (uint32_t)(rg.cap / T)]; };
   if (t == 0) {
     grab(nxt_tile, nxt_sub);
-    if (RG == 2) nxt_nv = region_nvalid(nxt_tile);
+    if (RG == 2) region_next(nxt_tile);
   }
   // GATHER: lanes 0-3 of wave 0 hold the next tile's descriptor.
   uint4 dreg = make_uint4(0u, 0u, 0u, 0u);
@@ -985,9 +979,13 @@ __device__ __forceinline__ void onesweep_body(
     if (t == 0) {
       s_tile = nxt_tile;
       s_sub = nxt_sub;
-      if (RG == 2) {
-        s_nv = nxt_nv;
-        s_tb = nxt_tb;
+      if (RG == 2 && nxt_tile >= 0) {
+        const uint32_t ct = (uint32_t)(rg.cap / T);
+        const uint32_t reg = (uint32_t)nxt_tile / ct;
+        const int64_t k = (int64_t)((uint32_t)nxt_tile - reg * ct);
+        const int64_t v = (int64_t)nxt_cnt - k * T;
+        s_nv = (int)(v < 0 ? 0 : (v < T ? v : T));
+        s_tb = region_base(reg, rg.cap) + k * T;
       }
     }
     if (GATHER && w == 0 && lane < 4) reinterpret_cast<uint4*>(&s_desc)[lane] = dreg;
@@ -1257,7 +1255,7 @@ __device__ __forceinline__ void onesweep_body(
 #endif
     if (t == 0) {  // in flight during the writes
       grab(nxt_tile, nxt_sub);
-      if (RG == 2) nxt_nv = region_nvalid(nxt_tile);
+      if (RG == 2) region_next(nxt_tile);
     }
 
     // emit: one staged record (tile position j, output slot delta + pos) to
