@@ -865,8 +865,7 @@ __device__ __forceinline__ void onesweep_body(
   __shared__ uint32_t nh[NEXT ? kSub * kBuckets : 1];  // next digit's sub-array histogram
   __shared__ uint64_t scan64[W];
   __shared__ uint32_t scan32[W];
-  __shared__ int32_t s_tile, s_sub, s_nv;
-  __shared__ int64_t s_tb;
+  __shared__ int32_t s_tile, s_sub;
   __shared__ uint32_t tile_lo[2];  // C16: low byte of the tile's first, last record
   __shared__ TileDesc s_desc;      // GATHER: where this tile's records are
 
@@ -959,12 +958,7 @@ __device__ __forceinline__ void onesweep_body(
   // The count is only consumed at the loop top, so the load's latency hides
   // behind this tile's write-out (computing the valid count right away made
   // wave 0, and with it the workgroup's closing barrier, wait for it).
-  uint32_t nxt_cnt = 0;  // RG = 2: the next tile's region count (its slots: region_slot)
-  auto region_next = [&](int tl) { nxt_cnt = tl < 0 ? 0u : rg.counts[(uint32_t)tl / (uint32_t)(rg.cap / T)]; };
-  if (t == 0) {
-    grab(nxt_tile, nxt_sub);
-    if (RG == 2) region_next(nxt_tile);
-  }
+  if (t == 0) grab(nxt_tile, nxt_sub);
   // GATHER: lanes 0-3 of wave 0 hold the next tile's descriptor.
   uint4 dreg = make_uint4(0u, 0u, 0u, 0u);
   auto fetch_desc = [&]() {
@@ -979,14 +973,6 @@ __device__ __forceinline__ void onesweep_body(
     if (t == 0) {
       s_tile = nxt_tile;
       s_sub = nxt_sub;
-      if (RG == 2 && nxt_tile >= 0) {
-        const uint32_t ct = (uint32_t)(rg.cap / T);
-        const uint32_t reg = (uint32_t)nxt_tile / ct;
-        const int64_t k = (int64_t)((uint32_t)nxt_tile - reg * ct);
-        const int64_t v = (int64_t)nxt_cnt - k * T;
-        s_nv = (int)(v < 0 ? 0 : (v < T ? v : T));
-        s_tb = region_base(reg, rg.cap) + k * T;
-      }
     }
     if (GATHER && w == 0 && lane < 4) reinterpret_cast<uint4*>(&s_desc)[lane] = dreg;
 #pragma unroll
@@ -1010,8 +996,22 @@ __device__ __forceinline__ void onesweep_body(
       }
       cur_sub = x;
     }
-    const int64_t tb = RG == 2 ? s_tb : (int64_t)tile * T;
-    const int nvalid = RG == 2 ? s_nv : (int)((m - tb) < T ? (m - tb) : T);
+    int64_t tb = (int64_t)tile * T;
+    int nvalid = (int)((m - tb) < T ? (m - tb) : T);
+    uint32_t rg_reg = 0, rg_k = 0;
+    if (RG == 2) {
+      // Tile k of region r: that region's slots [k * T, (k + 1) * T), all
+      // inside the buffer, so the record loads need no count: the count is
+      // loaded after them (below).  (Thread 0 fetching it with the next
+      // tile's id made the loop top wait for wave 0's write-out stores as
+      // well, vmcnt(0); loaded before the records, it held back half of
+      // their loads.)
+      const uint32_t tu = (uint32_t)__builtin_amdgcn_readfirstlane(tile);
+      const uint32_t ct = (uint32_t)(rg.cap / T);
+      rg_reg = tu / ct;
+      rg_k = tu - rg_reg * ct;
+      tb = region_base(rg_reg, rg.cap) + (int64_t)rg_k * T;
+    }
 
     Elem e[IPT];
     const int wbase = w * 64 * IPT + (int)lane;
@@ -1072,7 +1072,12 @@ __device__ __forceinline__ void onesweep_body(
 #pragma unroll
       for (int i = 0; i < IPT; ++i) {
         const int li = wbase + i * 64;
-        e[i] = li < nvalid ? load_elem_nt(in + tb + li) : Elem{0ull, 0ull};
+        e[i] = RG == 2 || li < nvalid ? load_elem_nt(in + tb + li) : Elem{0ull, 0ull};
+      }
+      if (RG == 2) {
+        __builtin_amdgcn_sched_barrier(0);
+        const int64_t v = (int64_t)rg.counts[rg_reg] - (int64_t)rg_k * T;
+        nvalid = (int)(v < 0 ? 0 : (v < T ? v : T));
       }
     }
 #ifdef LSB_OS_PROFILE
@@ -1255,7 +1260,6 @@ __device__ __forceinline__ void onesweep_body(
 #endif
     if (t == 0) {  // in flight during the writes
       grab(nxt_tile, nxt_sub);
-      if (RG == 2) region_next(nxt_tile);
     }
 
     // emit: one staged record (tile position j, output slot delta + pos) to
