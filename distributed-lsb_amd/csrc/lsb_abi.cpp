@@ -74,7 +74,7 @@ int lsb_rank_footprint(int64_t n_total, int num_ranks, int radix_bits, int with_
   const int64_t cap = record_capacity(per, (int)P);                // A and B (regional slots)
   const int64_t tiles = lsb::onesweep_tiles(per);
   const lsb::Chunking ch = lsb::make_chunking(per, 2 * 256);
-  int64_t b = 2 * (int64_t)rec_bytes((size_t)cap) + (with_recv ? rec : 0);
+  int64_t b = (with_recv ? 3 : 2) * (int64_t)rec_bytes((size_t)cap);  // A, B (and R) hold the same
   b += tiles * lsb::kBuckets * 4;                                   // os_status
   if (region_cap_for(per, (int)P) > 0)  // os_status2 and rg_buf of the regional first pass
     b += lsb::onesweep_tiles(region_cap_for(per, (int)P) * lsb::kRegions) * lsb::kBuckets * 4 +

@@ -376,7 +376,9 @@ int alloc_records(lsb_ctx* c, Rank& r) {
 // A may hold records by then and is not touched; the probe counts into a
 // histogram of its own, since a sort may hold one in r.os_hist.
 int alloc_third(lsb_ctx* c, Rank& r) {
-  const size_t per = (size_t)c->per;
+  // As many records as A and B: the hybrid permutes the three buffers, and
+  // the regional first pass writes into whichever one is B by then.
+  const size_t per = (size_t)r.cap;
   int K = r.placement_k > 0 ? placement_candidates((double)per * sizeof(Elem), 3) : 1;  // probed A and B only
   if (K <= 2) K = 1;
   if (K == 1 || !r.os_status) return rec_alloc(c, &r.R, per);

@@ -241,8 +241,10 @@ int onesweep_digits(lsb_ctx* c, Rank& r, const std::vector<int>& digits, int* pa
 // a word the host reads after the first pass, and the sort then starts over
 // from the input, which the first pass left in place.
 
+// The hybrid's passes may start with it too (its first pass on the lowest of
+// its top bytes; region_first's shift).
 bool region_applies(const lsb_ctx* c, const Rank& r) {
-  return c->region && !exchanging(c) && c->onesweep && c->os_split == 0 && c->hybrid == 0 && r.rg_cap > 0 &&
+  return c->region && !exchanging(c) && c->onesweep && c->os_split == 0 && r.rg_cap > 0 &&
          r.here == c->per && r.cap >= lsb::region_stride(r.rg_cap) * lsb::kRegions &&
          r.here <= lsb::kOnesweepMaxElems;
 }
@@ -255,14 +257,14 @@ lsb::RegionPass region_pass(Rank& r) {
   return rp;
 }
 
-// The sample (filed as the sort's count): *go = take the regional pass;
-// *seen = the key bits that vary in the sample.
-int region_sample(lsb_ctx* c, Rank& r, bool* go, uint64_t* seen) {
+// The sample (filed as the sort's count) of the byte the first pass sorts
+// on: *go = take the regional pass; *seen = the key bits that vary in it.
+int region_sample(lsb_ctx* c, Rank& r, int byte, bool* go, uint64_t* seen) {
   *go = false;
   if (!r.os_status2) return LSB_OK;  // allocated by onesweep_ensure
   {
     Timer t(c, &r, LSB_K_UPSWEEP);
-    HIP_TRY(lsb::launch_sample(r.A, r.here, 0, r.rg_buf + kRgHist,
+    HIP_TRY(lsb::launch_sample(r.A, r.here, byte * lsb::kDigitBits, r.rg_buf + kRgHist,
                                reinterpret_cast<uint64_t*>(r.rg_buf + kRgSpan), r.stream));
   }
   HIP_TRY(hipMemcpyAsync(r.rg_h + kRgHist, r.rg_buf + kRgHist, (size_t)(kRgWords - kRgHist) * sizeof(uint32_t),
@@ -286,15 +288,16 @@ int region_sample(lsb_ctx* c, Rank& r, bool* go, uint64_t* seen) {
   return LSB_OK;
 }
 
-// Pass 0 into the regional layout (r.A -> r.B, then they swap), counting
-// digit 1 into os_hist[1]; the overflow word's read-back is queued.
-int region_first(lsb_ctx* c, Rank& r, int* passes) {
+// The first pass into the regional layout (r.A -> r.B, then they swap) on
+// the byte at `shift`, counting the byte at next_shift into os_hist[1]; the
+// overflow word's read-back is queued.
+int region_first(lsb_ctx* c, Rank& r, int shift, int next_shift, int* passes) {
   const lsb::RegionPass rp = region_pass(r);
-  begin_pass(c, 0);
+  begin_pass(c, shift);
   lsb::OnesweepExtra x;
   x.region = &rp;
   x.region_mode = 1;
-  LSB_TRY(onesweep_launch(c, r, 0, lsb::kDigitBits, nullptr, r.os_hist + lsb::kOnesweepSubs * lsb::kBuckets, x));
+  LSB_TRY(onesweep_launch(c, r, shift, next_shift, nullptr, r.os_hist + lsb::kOnesweepSubs * lsb::kBuckets, x));
   ++*passes;
   HIP_TRY(hipMemcpyAsync(r.rg_h + kRgOvf, r.rg_buf + kRgOvf, sizeof(uint32_t), hipMemcpyDeviceToHost, r.stream));
   return LSB_OK;
@@ -395,6 +398,7 @@ struct LocalSort {
   int begin();
   int queue();
   int finish();
+  int hybrid_passes(size_t from);
   int classic();
   int first_hist(int byte, bool* skewed, bool* constant);
   int queue_err_word() {
@@ -444,6 +448,23 @@ int LocalSort::begin() {
     // Count the byte the first pass most likely sorts on (full 64-bit keys)
     // in the same read as the span, and queue its read-back beside the span's.
     const std::vector<int> guess = hybrid_bytes(~0ull, r.here);
+    region = false;
+    // The regional first pass for the hybrid's first byte pass (k >= 3: the
+    // pass that reads the layout must not be the segment pass).
+    if (guess.size() >= 3 && region_applies(c, r)) LSB_TRY(region_sample(c, r, guess[0], &region, &varying));
+    if (region) {  // every byte varies: the top bytes are the guess
+      c->last_first = LSB_FIRST_REGIONAL;
+      msd = guess;
+      X0 = r.A;
+      X1 = r.B;
+      X2 = r.R;
+      armed = true;
+      LSB_TRY(region_first(c, r, guess[0] * lsb::kDigitBits, guess[1] * lsb::kDigitBits, &passes));
+      r.B = X2;  // A is X1 now, B is X0: keep X0, write X2 next (hybrid_passes)
+      r.R = X0;
+      return LSB_OK;
+    }
+    varying = ~0ull;
     counted = guess.empty() ? 0 : guess[0];
     LSB_TRY(count_byte(c, r, counted, c->skip_constant));
     HIP_TRY(hipMemcpyAsync(r.os_hist_h, r.os_hist, sizeof(uint32_t) * lsb::kOnesweepSubs * lsb::kBuckets,
@@ -452,10 +473,10 @@ int LocalSort::begin() {
   } else {
     kind = kLsd;
     region = false;
-    if (region_applies(c, r)) LSB_TRY(region_sample(c, r, &region, &varying));
+    if (region_applies(c, r)) LSB_TRY(region_sample(c, r, 0, &region, &varying));
     if (region) {  // every digit varies: no span read
       c->last_first = LSB_FIRST_REGIONAL;
-      return region_first(c, r, &passes);
+      return region_first(c, r, 0, lsb::kDigitBits, &passes);
     }
     varying = ~0ull;
     LSB_TRY(count_byte(c, r, 0, c->skip_constant));
@@ -531,6 +552,33 @@ int LocalSort::queue() {
     kind = kDone;
     return queue_err_word();
   }
+  if (kind == kHybrid && region) {
+    region = false;
+    HIP_TRY(hipStreamSynchronize(r.stream));
+    if (r.rg_h[kRgOvf] == 0) {
+      digits = varying_bytes(~0ull);
+      r.os_halves = 1;
+      return hybrid_passes(1);
+    }
+    // A region overflowed: the kept input X0 and the usual start.
+    r.A = X0;
+    r.B = X1;
+    r.R = X2;
+    armed = false;
+    passes = 0;
+    c->pass_cursor = 0;
+    c->cur_pass = 0;
+    c->last_first = LSB_FIRST_REGIONAL_REDONE;
+    HIP_TRY(hipMemsetAsync(r.span, 0, 2 * sizeof(uint64_t), r.stream));
+    counted = msd[0];
+    LSB_TRY(count_byte(c, r, counted, c->skip_constant));
+    HIP_TRY(hipMemcpyAsync(r.os_hist_h, r.os_hist, sizeof(uint32_t) * lsb::kOnesweepSubs * lsb::kBuckets,
+                           hipMemcpyDeviceToHost, r.stream));
+    hist_queued = true;
+    if (c->skip_constant)
+      HIP_TRY(hipMemcpyAsync(r.span_h, r.span, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, r.stream));
+    varying = ~0ull;
+  }
   if (c->skip_constant) HIP_TRY(hipStreamSynchronize(r.stream));
   if (c->skip_constant) varying = r.span_h[0] & r.span_h[1];
   digits = varying_bytes(varying);
@@ -561,14 +609,22 @@ int LocalSort::queue() {
     kind = kDone;
     return queue_err_word();
   }
-  // The k passes: A -> B, then B <-> R; the input X0 is kept.  The last one
-  // also orders every segment inside its tile (SegPass) and k_segfix merges
-  // the segments split between tiles; LSB_OPT_HYBRID = 2, or the split stage,
-  // leaves the segments to a k_segsort pass instead.
-  X0 = r.A;
-  X1 = r.B;
-  X2 = r.R;
-  armed = true;
+  return hybrid_passes(0);
+}
+
+// The k passes: A -> B, then B <-> R; the input X0 is kept.  The last one
+// also orders every segment inside its tile (SegPass) and k_segfix merges
+// the segments split between tiles; LSB_OPT_HYBRID = 2, or the split stage,
+// leaves the segments to a k_segsort pass instead.  from = 1: the first pass
+// ran into the regional layout (begin), the second reads it.
+int LocalSort::hybrid_passes(size_t from) {
+  const int64_t m = r.here;
+  if (from == 0) {
+    X0 = r.A;
+    X1 = r.B;
+    X2 = r.R;
+    armed = true;
+  }
   for (int b : msd) pmask |= (uint64_t)(lsb::kBuckets - 1) << (b * lsb::kDigitBits);
   err = r.os_ctr + lsb::kOnesweepSubs + 1;
   fuse = c->hybrid == 1 && r.os_halves == 1 && !msd.empty();
@@ -581,12 +637,17 @@ int LocalSort::queue() {
   }
   HIP_TRY(hipMemsetAsync(err, 0, sizeof(uint32_t), r.stream));
   uint32_t* hist[2] = {r.os_hist, r.os_hist + lsb::kOnesweepSubs * lsb::kBuckets};
-  for (size_t i = 0; i < msd.size(); ++i) {
+  const lsb::RegionPass rp = from == 1 ? region_pass(r) : lsb::RegionPass();
+  for (size_t i = from; i < msd.size(); ++i) {
     const int shift = msd[i] * lsb::kDigitBits;
     const int next = i + 1 < msd.size() ? msd[i + 1] * lsb::kDigitBits : -1;
     begin_pass(c, shift);
     lsb::OnesweepExtra x;
     x.halves = r.os_halves;
+    if (from == 1 && i == 1) {
+      x.region = &rp;
+      x.region_mode = 2;
+    }
     if (fuse && i + 1 == msd.size()) {
       x.seg = &sp;
       seg_in = r.A;

@@ -175,3 +175,51 @@ def test_below_threshold_takes_the_count(lsb_built, monkeypatch):
         assert w.first_pass() == lsb_built.FIRST_COUNT
         ok, _ = w.verify()
         assert ok
+
+
+def test_hybrid_and_regional_sorts_share_a_context(lsb_built, small_regions):
+    """The hybrid permutes A, B and R; the regional first pass writes its
+    layout into whichever buffer is B by then, so R holds as many records as
+    A and B.  Hybrid and LSD sorts in turn on one context, each verified."""
+    L = lsb_built
+    n = (1 << 22) + 333
+    with L.World(n, ranks=1) as w:
+        for hybrid in (1, 0, 1, 0, 2, 0, 0):
+            w.set_option(L.OPT_HYBRID, hybrid)
+            w.generate()
+            w.my_sort()
+            ok, bad = w.verify()
+            assert ok and bad == -1, hybrid
+            if hybrid == 0:
+                assert w.first_pass() == L.FIRST_REGIONAL
+
+
+@pytest.mark.parametrize("hybrid", [1, 2])
+def test_hybrid_starts_with_the_regional_pass(lsb_built, oracle_mod, small_regions, hybrid):
+    """The hybrid's first byte pass (the lowest of its top bytes) into the
+    regional layout, its second reading it; bit-exact, then an overflow the
+    sample misses (the kept input sorted the usual way)."""
+    L = lsb_built
+    n = (1 << 22) + 4097
+    a = _uniform(n, 22 + hybrid)
+    with L.World(n, ranks=1) as w:
+        w.set_option(L.OPT_HYBRID, hybrid)
+        w.scatter_global(a)
+        w.my_sort()
+        assert w.first_pass() == L.FIRST_REGIONAL
+        assert np.array_equal(w.gather_global(), oracle_mod.stable_sort(a))
+        # 2^22 records: k = 3 top bytes (5, 6, 7); crowd byte 5 = 0x21 in
+        # sub-array 6's tiles that the sample (tile g * TT / 256 for g < 256)
+        # does not read.
+        b = _uniform(n, 5)
+        k = b["key"]
+        tile = np.arange(n) // 4096
+        TT = (n + 4095) // 4096
+        sampled = np.array(sorted({g * TT // 256 for g in range(256)}))
+        lo, hi = 6 * TT // 8 * 4096, 7 * TT // 8 * 4096
+        sel = np.flatnonzero((np.arange(n) >= lo) & (np.arange(n) < hi) & ~np.isin(tile, sampled))[:9000]
+        k[sel] = (k[sel] & ~np.uint64(0xFF << 40)) | np.uint64(0x21 << 40)
+        w.scatter_global(b)
+        w.my_sort()
+        assert w.first_pass() == L.FIRST_REGIONAL_REDONE
+        assert np.array_equal(w.gather_global(), _stable(b))
