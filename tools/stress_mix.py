@@ -74,6 +74,8 @@ def main():
     ap.add_argument("--seconds", type=float, default=240)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--max-log2", type=int, default=27)
+    ap.add_argument("--trace", action="store_true", help="print each configuration before its sort")
+    ap.add_argument("--stop-on-error", action="store_true", help="end at the first wrong sort or error")
     a = ap.parse_args()
     rng = random.Random(a.seed)
     t_end = time.time() + a.seconds
@@ -99,6 +101,8 @@ def main():
         desc = (f"iter {it}: n={n} P={P} bits={bits} dist={dist} split={split} hybrid={hybrid} "
                 f"gather={gather} vmm={vmm} region_min={region_min}")
         t0 = time.time()
+        if a.trace:  # the configuration before the sort: a fault kills the process mid-sort
+            print(f"begin {desc}", flush=True)
         try:
             with lsbsort.World(n, ranks=P, radix_bits=bits) as w:
                 w.set_option(lsbsort.OPT_ONESWEEP_SPLIT, split)
@@ -122,6 +126,10 @@ def main():
             ok, first, srt, form = False, str(e), False, -1
         if not (ok and srt):
             bad += 1
+            if a.stop_on_error:
+                print(f"{desc} first_pass={form} verify={ok} first_bad={first} sorted={srt}", flush=True)
+                print(f"done: {bad} of {it + 1} sorts wrong (stopped at the first)", flush=True)
+                sys.exit(1)
         print(f"{desc} first_pass={form} verify={ok} first_bad={first} sorted={srt} "
               f"ms={(time.time() - t0) * 1e3:.0f}", flush=True)
         it += 1
