@@ -196,6 +196,14 @@ void lsb_destroy(lsb_ctx_t* c) {
   (void)lsb_sync(c);
   os_profile_report();
 #endif
+  // Every rank's streams first: a loopback rank's stream reads the other
+  // ranks' buffers (exchange copies), and VMM record buffers are unmapped
+  // without the implicit device synchronisation hipFree has.
+  for (Rank& r : c->ranks) {
+    (void)hipSetDevice(r.dev);
+    if (r.stream) (void)hipStreamSynchronize(r.stream);
+    if (r.pstream) (void)hipStreamSynchronize(r.pstream);
+  }
   for (Rank& r : c->ranks) free_rank(r);
   for (auto& e : c->event_pool) (void)hipEventDestroy(e.second);
   if (c->comm) (void)ncclCommDestroy(c->comm);

@@ -172,6 +172,9 @@ void rec_free(void* p) {
     (void)hipFree(p);
     return;
   }
+  // hipFree waits for the device; unmapping does not: a kernel or copy still
+  // using the pieces would fault.
+  (void)hipDeviceSynchronize();
   vmm_release(b, b.piece);
 }
 

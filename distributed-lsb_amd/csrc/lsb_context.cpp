@@ -121,10 +121,9 @@ int init_rank(lsb_ctx* c, Rank& r, int rank, int dev) {
 }
 
 void free_rank(Rank& r) {
-  if (r.stream) {
-    (void)hipSetDevice(r.dev);
-    (void)hipStreamSynchronize(r.stream);
-  }
+  (void)hipSetDevice(r.dev);
+  if (r.stream) (void)hipStreamSynchronize(r.stream);
+  if (r.pstream) (void)hipStreamSynchronize(r.pstream);  // placements read R and write B
   for (void* p : r.ipc_opened) (void)hipIpcCloseMemHandle(p);
   (void)hipFree(r.peer_base);
   (void)hipFree(r.split_state);
