@@ -997,9 +997,10 @@ def main():
         "exchange_bytes_per_step": xbytes // a.steps if N > 1 or a.force_exchange else 0,
         "exchange_roofline": xroof,
         "placement": dict(placement, record_alloc=os.environ.get("LSB_RECORD_ALLOC", "vmm 1 GiB pieces"),
-                          basis="rank 0's A and B: built from 1 GiB VMM pieces (no probe: candidates 0); with "
-                                "LSB_PLACEMENT_CANDIDATES = K > 2, chosen at context creation among K buffers "
-                                "by one timed k_onesweep pass between every ordered pair; ms per pass, mean "
+                          basis="rank 0's A and B: built from 1 GiB VMM pieces, chosen at context creation "
+                                "among K candidate buffers (by default 4 for buffers of >= 4 GiB; "
+                                "LSB_PLACEMENT_CANDIDATES = K; candidates 0: no probe) by one timed "
+                                "k_onesweep pass between every ordered pair; ms per pass, mean "
                                 "of both directions: the kept pair, the first two allocated, the slowest "
                                 "(lsb_get_placement; DESIGN.md 4)"),
         "device_memory": mem,

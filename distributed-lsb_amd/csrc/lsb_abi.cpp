@@ -70,7 +70,6 @@ int lsb_rank_footprint(int64_t n_total, int num_ranks, int radix_bits, int with_
     return fail(LSB_ERR_UNSUPPORTED, "lsb_rank_footprint", "radix_bits must be 8, 16 or 64");
   const int64_t P = num_ranks, per = div_ceil(n_total, num_ranks);
   const int64_t nb = radix_bits == 64 ? lsb::kBuckets : (int64_t)1 << radix_bits;
-  const int64_t rec = rec_bytes((size_t)per);
   const int64_t cap = record_capacity(per, (int)P);                // A and B (regional slots)
   const int64_t tiles = lsb::onesweep_tiles(per);
   const lsb::Chunking ch = lsb::make_chunking(per, 2 * 256);
@@ -90,10 +89,10 @@ int lsb_rank_footprint(int64_t n_total, int num_ranks, int radix_bits, int with_
          (int64_t)(P * 8) * lsb::kSplitCands * 8 * (P + 1);         // merge_path, split_* (8 slices)
   *bytes = b;
   if (probe_bytes) {
-    int K = 0;
-    if (const char* e = getenv("LSB_PLACEMENT_CANDIDATES")) K = atoi(e);
-    K = std::min(K, 8);
-    *probe_bytes = K > 2 && rec >= ((int64_t)1 << 30) ? (K - 2) * rec : 0;
+    const int64_t cap_rec = rec_bytes((size_t)cap);  // a candidate holds as many records as A
+    double share = 0.0;
+    const int K = placement_request((double)cap_rec, &share);
+    *probe_bytes = K > 2 && cap_rec >= ((int64_t)1 << 30) ? (K - 2) * cap_rec : 0;
   }
   return LSB_OK;
 }

@@ -178,31 +178,35 @@ void rec_free(void* p) {
   vmm_release(b, b.piece);
 }
 
-// ---- record buffers A and B: the optional placement probe -----------------------
+// ---- record buffers A and B: the placement probe ---------------------------------
 // Before round 5 the record buffers were hipMalloc'd, and how fast an LSD pass
 // streamed between two of them depended on where the driver placed them: the
 // pass ran at 6.7-7.3 ms between pairs allocated in one process
 // (profiles/r04/v5_pick.log).  Round 4 therefore chose A and B among 8
 // candidate buffers by timing one k_onesweep pass between every ordered pair
 // (~0.7 s and 128 GiB at context creation at 2^30 records).  Buffers built
-// from 1 GiB VMM pieces (rec_alloc) run every pass at 6.69-6.71 ms on average
-// in each of five fresh processes with no probe, where hipMalloc'd pairs ran
-// at 6.71, 6.99 and 7.27 (profiles/r05/alloc_sweep.log), so the probe is now
-// opt-in: LSB_PLACEMENT_CANDIDATES = K > 2 (at most 8) still tries K
-// candidates for A and B (and min(K, 3) for R), for buffers of at least
-// 1 GiB, as many as fit in 90 % of the free memory, and never when another
-// rank of this context shares the device (its timings would be the other
-// rank's too, and the candidates its memory).
+// from 1 GiB VMM pieces (rec_alloc) narrowed the spread, and round 5 first
+// turned the probe off.  They did not remove it: a buffer of pieces can still
+// be a slow destination as a whole (tools/kbench/pairbw2.hip: 8-piece buffers
+// 3.7-3.9 against 2.9 ms, 16-piece 5.71-5.96 ms for the LSD write pattern;
+// profiles/r05/region/pairbw2_*.log), which left one pass direction 2-5 % slow on about
+// half the boxes.  Four candidates of VMM pieces take the sort from
+// 53.96-56.26 ms to 53.68-54.08 (profiles/r05/probe/, 24 fresh processes on
+// 3 boxes), so the probe is on again by default, smaller: 4 candidates, for
+// buffers of at least 4 GiB, within half the free memory (~0.2 s and two
+// buffers more at creation); LSB_PLACEMENT_CANDIDATES = K sets K (0: off; at
+// most 8, within 90 %).  Never when another rank of this context shares the
+// device (its timings would be the other rank's too, and the candidates its
+// memory).
 namespace {
 
 // How many candidate buffers of `bytes` to try, at most `cap` (<= 2: no probing).
 int placement_candidates(double bytes, int cap) {
-  int K = 0;
-  if (const char* e = getenv("LSB_PLACEMENT_CANDIDATES")) K = atoi(e);
-  K = std::min(K, cap);
+  double share = 0.0;
+  int K = std::min(placement_request(bytes, &share), cap);
   size_t free_b = 0, total_b = 0;
   if (K > 2 && bytes >= (double)(1ull << 30) && hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
-    while (K > 2 && K * bytes > 0.9 * (double)free_b) --K;
+    while (K > 2 && K * bytes > share * (double)free_b) --K;
   } else {
     (void)hipGetLastError();
     K = 2;
@@ -285,6 +289,15 @@ int probe_check(Rank& r) {
   HIP_TRY(hipMemset(r.os_status, 0, (size_t)lsb::onesweep_tiles(r.here) * lsb::kBuckets * sizeof(uint32_t)));
   r.os_epoch = 0;
   return fail(LSB_ERR_HIP, "placement probe", "k_onesweep look-back timed out");
+}
+
+int placement_request(double bytes, double* free_share) {
+  if (const char* e = getenv("LSB_PLACEMENT_CANDIDATES")) {
+    *free_share = 0.9;
+    return std::min(atoi(e), 8);
+  }
+  *free_share = 0.5;
+  return bytes >= kProbeMinBytes ? kDefaultCandidates : 0;
 }
 
 int64_t region_min() {

@@ -296,6 +296,14 @@ int max_chunks_for_device(int dev);
 int64_t region_min();
 int64_t region_cap_for(int64_t per, int P);
 int64_t record_capacity(int64_t per, int P);
+// The placement probe's request for record buffers of `bytes`, before the
+// free-memory cap: candidates K (<= 2: no probe) and the share of the free
+// memory the K buffers may take.  LSB_PLACEMENT_CANDIDATES = K sets it (at
+// most 8, 90 %); unset, buffers of at least kProbeMinBytes get
+// kDefaultCandidates within half the free memory.
+constexpr int kDefaultCandidates = 4;
+constexpr double kProbeMinBytes = double(int64_t(4) << 30);
+int placement_request(double bytes, double* free_share);
 int alloc_records(lsb_ctx* c, Rank& r);  // A and B (placement-calibrated)
 int alloc_third(lsb_ctx* c, Rank& r);    // R, placed against A and B
 int init_rank(lsb_ctx* c, Rank& r, int rank, int dev);

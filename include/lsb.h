@@ -166,10 +166,12 @@ int64_t lsb_here(int64_t n_total, int num_ranks, int rank);      /* clamp(n - r*
  * output again; one exchange per sort instead of 64 / radix_bits.
  * Device memory per rank: lsb_rank_footprint (A and B here; R, the receive
  * buffer, at the first exchange or hybrid sort; record buffers of >= 1 GiB
- * are whole 1 GiB VMM pieces).  With LSB_PLACEMENT_CANDIDATES = K > 2 a
- * rank alone on its device also holds K - 2 more record buffers while its
- * placement probe runs (lsb_get_placement), as many as fit in 90 % of the
- * free memory at that moment. */
+ * are whole 1 GiB VMM pieces).  While its placement probe runs
+ * (lsb_get_placement) a rank alone on its device holds K - 2 more record
+ * buffers for a moment: by default K = 4 for buffers of >= 4 GiB, as many as
+ * fit in half the free memory at that moment (2^30 records: 34 GiB more for
+ * ~0.2 s); LSB_PLACEMENT_CANDIDATES = K sets K (0: no probe; at most 8,
+ * within 90 % of the free memory). */
 int  lsb_create(lsb_ctx_t** ctx, int64_t n_total, int num_ranks,
                 const int* dev_ids, int radix_bits);
 /* HIP devices this process can see (hipGetDeviceCount; 0 when there is
@@ -333,15 +335,15 @@ int  lsb_get_pass_exchange(lsb_ctx_t* ctx, int pass, int64_t* bytes, double* wir
 
 /* How the local rank's record buffers A and B were placed.  Record buffers of
  * at least 1 GiB are built from 1 GiB physical pieces (HIP virtual memory;
- * LSB_RECORD_ALLOC=malloc: hipMalloc), which run every pass at the same speed
- * in every process.  The round-4 placement probe remains as an
- * option: with LSB_PLACEMENT_CANDIDATES = K > 2 (at most 8) a rank whose
- * buffers hold >= 1 GiB and that shares its device with no other rank of the
- * context allocates K candidate buffers (as many as fit in 90 % of the free
- * memory; a transient peak of K record buffers, see lsb_rank_footprint),
- * times one k_onesweep pass over uniform keys between every ordered pair,
- * keeps the pair fastest both ways and frees the rest.  candidates = 0: no
- * probe ran.  Milliseconds per pass, mean of both directions: the chosen
+ * LSB_RECORD_ALLOC=malloc: hipMalloc).  Such a buffer can still be a slow
+ * pass destination as a whole, so a rank whose buffers hold
+ * >= 4 GiB and that shares its device with no other rank of the context
+ * allocates 4 candidate buffers (LSB_PLACEMENT_CANDIDATES = K: K of them, at
+ * most 8, for buffers of >= 1 GiB; 0: none), as many as fit in half the
+ * free memory (90 % when K is set; a transient peak of K record buffers,
+ * see lsb_rank_footprint), times one k_onesweep pass over uniform keys
+ * between every ordered pair, keeps the pair fastest both ways and frees
+ * the rest.  candidates = 0: no probe ran.  Milliseconds per pass, mean of both directions: the chosen
  * pair, the first two buffers allocated (what a plain allocation would have
  * kept) and the slowest pair. */
 int  lsb_get_placement(lsb_ctx_t* ctx, int rank, int* candidates, double* chosen_ms,

@@ -343,7 +343,8 @@ def test_rank_footprint_model(lsb_built, monkeypatch):
     """lsb_rank_footprint (host arithmetic): record buffers rounded up to whole
     1 GiB VMM pieces (hipMalloc'd ones are not), R only with an exchange or
     the hybrid, 4 B of look-back row per bucket per 4096-record tile, and the
-    placement probe's K - 2 extra candidates only when asked for."""
+    placement probe's K - 2 extra candidates (by default 4 candidates for
+    buffers of at least 4 GiB; LSB_PLACEMENT_CANDIDATES = K sets K)."""
     L = lsb_built
     gib = 1 << 30
     monkeypatch.delenv("LSB_PLACEMENT_CANDIDATES", raising=False)
@@ -358,9 +359,11 @@ def test_rank_footprint_model(lsb_built, monkeypatch):
     slots = 2048 * 130 * 4096
     f = L.rank_footprint(n, 1, 8)
     assert 0 <= f["bytes"] - 34 * gib - rows - (slots // 4096) * 256 * 4 < 64 << 20
+    assert f["probe_bytes"] == 2 * 17 * gib  # the default probe: 4 candidates of 17 pieces
     monkeypatch.setenv("LSB_REGION_MIN", str(1 << 40))  # no regional slots from here on
     f = L.rank_footprint(n, 1, 8)
-    assert f["probe_bytes"] == 0 and 0 <= f["bytes"] - 32 * gib - rows < 64 << 20
+    assert f["probe_bytes"] == 2 * 16 * gib and 0 <= f["bytes"] - 32 * gib - rows < 64 << 20
+    assert L.rank_footprint(n // 8, 1, 8)["probe_bytes"] == 0  # 2 GiB buffers: no default probe
     extra = L.rank_footprint(n, 1, 8, with_recv=True)["bytes"] - f["bytes"]
     assert 16 * gib <= extra < 16 * gib + (64 << 20)  # R, and the gathered passes' tile descriptors
     ragged = L.rank_footprint(n + 12345, 1, 8)["bytes"]
@@ -368,6 +371,8 @@ def test_rank_footprint_model(lsb_built, monkeypatch):
     monkeypatch.setenv("LSB_RECORD_ALLOC", "malloc")
     assert L.rank_footprint(n + 12345, 1, 8)["bytes"] - f["bytes"] < 1 << 20
     monkeypatch.delenv("LSB_RECORD_ALLOC")
+    monkeypatch.setenv("LSB_PLACEMENT_CANDIDATES", "0")
+    assert L.rank_footprint(n, 1, 8)["probe_bytes"] == 0
     monkeypatch.setenv("LSB_PLACEMENT_CANDIDATES", "8")
     assert L.rank_footprint(n, 1, 8)["probe_bytes"] == 6 * 16 * gib
     assert L.rank_footprint(1 << 20, 1, 8)["probe_bytes"] == 0  # buffers under 1 GiB: no probe

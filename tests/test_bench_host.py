@@ -205,8 +205,8 @@ def test_wrong_peer_output_fails_the_run():
 def test_eight_rank_memory_fits_the_device(candidates):
     """at the driver's N = 8 (2^30 records per GPU) one
     rank's A, B, R, look-back rows and tables fit one MI355X (288 GB, the
-    dry run's stand-in for lsb_device_memory), also with the optional
-    placement probe's 8 candidates (LSB_PLACEMENT_CANDIDATES=8), and a
+    dry run's stand-in for lsb_device_memory), with the placement probe's
+    default 4 candidates and with 8 (LSB_PLACEMENT_CANDIDATES=8), and a
     failing peer extra keeps the headline line."""
     env = dict(os.environ)
     env.pop("LSB_PLACEMENT_CANDIDATES", None)
@@ -220,5 +220,5 @@ def test_eight_rank_memory_fits_the_device(candidates):
     m = out["device_memory"]
     gib = 1 << 30
     assert 48 * gib <= m["bytes"] < 49 * gib  # A, B, R of 16 GiB each + 1/64 look-back rows
-    assert m["probe_bytes"] == (6 * 16 * gib if candidates else 0)
+    assert m["probe_bytes"] == (6 if candidates else 2) * 16 * gib
     assert m["device_bytes"] == 288 * 10**9 and m["fits"] and m["peak_frac"] < 0.9

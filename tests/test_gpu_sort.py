@@ -767,12 +767,12 @@ def test_harness_rccl_ranks_share_gpu(lsb_built, ref_vectors, n, P, extra):
     assert printed == [f"A[{i}] = ({k},{v})" for i, k, v in case["input"] + case["output"]]
 
 
-# ------------------------------------- record buffers and the opt-in probe
+# ------------------------------------- record buffers and the placement probe
 @pytest.mark.parametrize("alloc", ["vmm", "malloc"])
 def test_record_buffers_and_opt_in_probe(lsb_built, monkeypatch, alloc):
     """Record buffers of >= 1 GiB are built from 1 GiB VMM pieces
     (LSB_RECORD_ALLOC=malloc: hipMalloc) and no placement probe runs by
-    default (lsb_get_placement: 0 candidates).  LSB_PLACEMENT_CANDIDATES=8
+    default for buffers under 4 GiB (lsb_get_placement: 0 candidates).  LSB_PLACEMENT_CANDIDATES=8
     still picks A and B among 8 candidate buffers by a timed pass, and R
     among 3.  Every form sorts the same (verified on device), the local LSD
     passes, the hybrid (R) and the forced exchange (R)."""
@@ -819,6 +819,30 @@ def test_record_buffers_and_opt_in_probe(lsb_built, monkeypatch, alloc):
     # P logical ranks on one device never probe (the advisor's shared-device case)
     with lsb_built.World(4 * n, ranks=4) as w:
         assert all(w.placement(r)["candidates"] == 0 for r in range(4))
+
+
+def test_default_probe_on_large_buffers(lsb_built, monkeypatch):
+    """Buffers of at least 4 GiB (2^28 records) take the placement probe by
+    default: 4 candidates of VMM pieces, the pair fastest both ways kept
+    (DESIGN.md §4), and the sorts that follow, LSD and hybrid (R placed
+    among 3 against B), verify.  LSB_PLACEMENT_CANDIDATES=0 turns it off."""
+    monkeypatch.delenv("LSB_PLACEMENT_CANDIDATES", raising=False)
+    monkeypatch.delenv("LSB_RECORD_ALLOC", raising=False)
+    n = 1 << 28
+    with lsb_built.World(n, ranks=1) as w:
+        p = w.placement()
+        assert p["candidates"] == 4, p
+        assert 0 < p["chosen_ms"] <= p["first_pair_ms"] <= p["worst_ms"], p
+        w.generate()
+        w.my_sort()
+        assert w.verify() == (True, -1)
+        w.set_option(lsb_built.OPT_HYBRID, 1)
+        w.generate()
+        w.my_sort()
+        assert w.verify() == (True, -1)
+    monkeypatch.setenv("LSB_PLACEMENT_CANDIDATES", "0")
+    with lsb_built.World(n, ranks=1) as w:
+        assert w.placement()["candidates"] == 0
 
 
 @pytest.mark.parametrize("P,bits,hybrid", [(1, 8, 0), (1, 8, 1), (2, 16, 0), (8, 8, 0), (8, 16, 0), (4, 64, 0)])

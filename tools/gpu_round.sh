@@ -7,6 +7,7 @@
 #   bench     bench.py at N = 1 (live PMC traffic + CPU baseline)
 #   n2        bench.py --gpus 2 with no launcher over RCCL's socket transport
 #             (two rank processes on the one GPU: the N > 1 code path, not a speed)
+#   n2big     the same at 2^28 records per rank (the placement probe runs in each rank)
 #   n4zipf    the same at N = 4 with Zipf keys
 #   n8        bench.py --gpus 8 over RCCL sockets at 2^22 records per rank (the driver's N = 8 flow)
 #   table     tools/table_runs.sh: the DESIGN.md §4 table on this box
@@ -45,6 +46,10 @@ for s in $RUN; do
       timeout -k 10 400 python -u bench.py --gpus 2 --transport rccl-sockets --n-per-gpu 67108864 \
         --steps 2 --warmup 1 --no-cpu-baseline > $O/bench_n2.log 2>&1 || fail n2 $O/bench_n2.log
       tail -1 $O/bench_n2.log | cut -c1-400 ;;
+    n2big)  # N = 2 at 2^28 records per rank: 4 GiB buffers, so each rank runs the placement probe
+      timeout -k 10 400 python -u bench.py --gpus 2 --transport rccl-sockets --n-per-gpu 268435456 \
+        --steps 2 --warmup 1 --no-cpu-baseline > $O/bench_n2big.log 2>&1 || fail n2big $O/bench_n2big.log
+      tail -1 $O/bench_n2big.log | cut -c1-400 ;;
     n4zipf)
       timeout -k 10 400 python -u bench.py --gpus 4 --transport rccl-sockets --dist zipf \
         --n-per-gpu 16777216 --steps 2 --warmup 1 --no-cpu-baseline > $O/bench_n4_zipf.log 2>&1 \
