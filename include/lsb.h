@@ -356,9 +356,11 @@ int  lsb_get_placement(lsb_ctx_t* ctx, int rank, int* candidates, double* chosen
  * receive buffer R when with_recv (any exchange: num_ranks > 1 or forced; the
  * hybrid local sort), the single-read passes' look-back rows (4 B per bucket
  * per 4096-record tile), the gathered passes' tile descriptors (exchanges),
- * and the count and plan tables.  *probe_bytes: what the optional placement
- * probe (LSB_PLACEMENT_CANDIDATES, read from the environment now) holds on
- * top while it runs, at most; 0 when no probe would run.  A model of
+ * and the count and plan tables.  *probe_bytes: what the placement probe
+ * (by default 4 candidates for buffers of >= 4 GiB; LSB_PLACEMENT_CANDIDATES,
+ * read from the environment now) holds on top while it runs, at most (a rank
+ * that shares its device with another rank of its context runs none); 0 when
+ * no probe would run.  A model of
  * init_rank's allocations, checked against the device's own free-memory
  * count by tests/test_footprint_gpu.py. */
 int  lsb_rank_footprint(int64_t n_total, int num_ranks, int radix_bits, int with_recv,
