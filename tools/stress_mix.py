@@ -14,7 +14,9 @@ argsort.  Record buffers come from VMM pieces of a drawn size (2 MiB,
 regional first pass (LSB_OPT_REGION_FIRST) starts at a drawn size (2^16
 records or the default 2^27), and some host-made keys crowd one digit-0
 bucket of one sub-array (the regions the sample may miss, so some sorts
-overflow one and start over); each line names how the sort began.  Runs
+overflow one and start over); each line names how the sort began.  One
+draw in three sets LSB_PLACEMENT_CANDIDATES=4 (the placement probe for the
+P = 1 buffers of >= 1 GiB, built from the drawn pieces), the others 0.  Runs
 until --seconds have passed; one line per iteration.
 
     python tools/stress_mix.py --seconds 240 --seed 1
@@ -98,8 +100,11 @@ def main():
         # buffer at these sizes), or the default 1 GiB (hipMalloc below it)
         vmm = rng.choice((2, 64, 1024, 1024))
         os.environ["LSB_VMM_CHUNK_MIB"] = str(vmm)
+        # the placement probe: off, or 4 candidates (K set: buffers of >= 1 GiB)
+        probe = rng.choice((0, 0, 4))
+        os.environ["LSB_PLACEMENT_CANDIDATES"] = str(probe)
         desc = (f"iter {it}: n={n} P={P} bits={bits} dist={dist} split={split} hybrid={hybrid} "
-                f"gather={gather} vmm={vmm} region_min={region_min}")
+                f"gather={gather} vmm={vmm} region_min={region_min} probe={probe}")
         t0 = time.time()
         if a.trace:  # the configuration before the sort: a fault kills the process mid-sort
             print(f"begin {desc}", flush=True)
