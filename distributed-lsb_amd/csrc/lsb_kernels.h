@@ -128,11 +128,17 @@ hipError_t onesweep_profile(unsigned long long* out10, bool reset);
 // runs that cross a tile boundary can leave a segment split between two
 // tiles, and launch_segfix merges those from the pass's input, its look-back
 // rows and base (workgroup 0 writes base[x * 256 + b] = the first output slot
-// of bucket b's sub-array x records).  *err |= 1 when a segment inside a
-// tile holds more than kSegMax records, or a crossing run more than kSegCap
-// (4 * kSegCap when runs average over 64 records) on one side of its
-// boundary or spans a whole tile (the runtime then runs k_segsort on the
-// output).
+// of bucket b's sub-array x records).  *err |= 1 (launch_segfix) when a
+// crossing run holds more than kSegCap records (4 * kSegCap when runs
+// average over 64 records) on one side of its boundary or spans a whole
+// tile: that boundary is left alone, the output is still a permutation sorted
+// by pmask, and the runtime runs k_segsort on it.  *err |= 2 (this pass)
+// when a segment inside a tile holds more than kSegMax records: its records'
+// slots came from walks cut at kSegMax and may collide, so the output is not
+// a permutation, and the runtime sorts the kept input with the LSD passes
+// (stress seed 19: k_segsort over such an output, its holes holding stale
+// records that split the long segments, found nothing too long and kept a
+// wrong result).
 constexpr int kSegCap = 256;
 struct SegPass {
   uint64_t pmask = 0;

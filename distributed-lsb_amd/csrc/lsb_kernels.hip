@@ -1373,7 +1373,8 @@ __device__ __forceinline__ void onesweep_body(
               ++k;
             }
             too_long |= k == khi && khi < nvalid;
-            if (too_long) atomicOr(seg.err, 1u);
+            // 2: this tile's slots may collide (not a permutation, SegPass).
+            if (too_long) atomicOr(seg.err, 2u);
             pos = sfirst + (int)(less + eqb);
           }
         }

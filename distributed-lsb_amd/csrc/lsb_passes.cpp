@@ -684,13 +684,18 @@ int LocalSort::finish() {
     *v = r.os_err_h[1];
     return LSB_OK;
   };
-  bool sorted = false;
+  bool sorted = false, a_valid = true;
   if (fuse) {  // its error word's read-back was queued after k_segfix
     uint32_t e = 0;
     LSB_TRY(sync_err(&e));
     sorted = e == 0;
+    // Bit 2: a segment of the fused pass ran past kSegMax inside its tile,
+    // so r.A is not a permutation (SegPass, lsb_kernels.h): straight to the
+    // LSD passes over the kept input.  Bit 1 alone: k_segfix left a
+    // boundary, and k_segsort finishes r.A.
+    a_valid = (e & 2u) == 0;
   }
-  if (!sorted) {
+  if (!sorted && a_valid) {
     // k_segsort: r.A is stably sorted by pmask (the fused pass's segments
     // too, in or out of order).
     HIP_TRY(hipMemsetAsync(err, 0, sizeof(uint32_t), r.stream));

@@ -10,8 +10,8 @@ The output must be the reference's: the stable sort by key
 :722-737 checks exactly that), bit for bit against the oracle.  Sizes straddle
 k_segsort's 4096-record tiles and the choice of k; distributions include the
 skewed ones that take the LSD passes directly, and keys whose segments run
-past k_segsort's 1024-record limit, where the sort must redo the kept input
-with the LSD passes.
+past the segment sorts' kSegMax (64 records), where the sort must redo the
+kept input with the LSD passes (without trusting the fused pass's output).
 """
 import numpy as np
 import pytest
@@ -171,7 +171,47 @@ def test_long_segments_fall_back_to_lsd(lsb_built, oracle_mod, bases):
     a["val"] = np.arange(n, dtype=np.uint64)
     out, (lp, _, _), _ = _sort(lsb_built, a)
     assert np.array_equal(out, oracle_mod.stable_sort(a))
-    assert lp == 3 + 1 + 8  # 3 byte passes + the failed segment sorts + the LSD passes
+    # 3 byte passes, then (the fused pass found a segment past kSegMax inside
+    # a tile: its output is no permutation) straight to the 8 LSD passes
+    assert lp == 3 + 8
+    out, (lp, _, _), _ = _sort(lsb_built, a, mode=2)
+    assert np.array_equal(out, oracle_mod.stable_sort(a))
+    assert lp == 3 + 1 + 8  # mode 2: the byte passes, the failed k_segsort, the LSD passes
+
+
+def _stress_seed19_iter3258(n):
+    """The input that made `tools/stress_mix.py --seed 19 --max-log2 29` fail
+    at iteration 3258 (P = 2, whole key, hybrid 1; its rank 0 block alone
+    fails the same way at P = 1), rebuilt from the draws its thinned_keys
+    made (`tools/stress_replay.py`): uniform bytes 0-2 and 4, bytes 3 and 5
+    constant, bytes 6 and 7 each from a pool of two values."""
+    g = np.random.default_rng(10821365)
+    full = 693_391
+    k = g.integers(0, 2**64 - 1, full, dtype=np.uint64)
+    for b, c in ((3, 174), (5, 227)):
+        sh = np.uint64(8 * b)
+        k = (k & ~(np.uint64(0xFF) << sh)) | (np.uint64(c) << sh)
+    for b in (6, 7):
+        sh = np.uint64(8 * b)
+        pool = g.integers(0, 256, 2, dtype=np.uint64)
+        k = (k & ~(np.uint64(0xFF) << sh)) | (pool[g.integers(0, pool.size, full)] << sh)
+    a = np.zeros(full, dtype=DT)
+    a["key"] = k
+    a["val"] = np.arange(full, dtype=np.uint64)
+    return a[:n].copy()
+
+
+def test_fused_pass_with_long_segments_stress_seed19(lsb_built, oracle_mod):
+    """Round 5's stress found it: the fused pass (mode 1) over
+    segments of ~340 records computed their slots from walks cut at kSegMax,
+    so records collided and stale ones filled the holes; k_segsort, run on
+    that output, found the long segments cut short by the stale records and
+    kept a wrong result.  Now such a pass sends the sort straight to the LSD
+    passes over the kept input: 3 byte passes + 6 (bytes 3 and 5 constant)."""
+    a = _stress_seed19_iter3258(346_696)
+    out, (lp, _, _), _ = _sort(lsb_built, a)
+    assert np.array_equal(out, oracle_mod.stable_sort(a))
+    assert lp == 3 + 6
 
 
 def test_constant_top_byte_takes_lsd(lsb_built, oracle_mod):
