@@ -120,9 +120,9 @@ typedef struct lsb_ctx lsb_ctx_t;
                                       (the stable sort by key) from k passes over HBM instead of up
                                       to 8.  Skewed keys (one bucket of the first byte over 1/32 of
                                       the records) take the LSD passes; runs too long for k_segfix
-                                      take k_segsort, and segments longer than 1024 records make
-                                      the sort redo the kept input by the LSD passes.  Needs a
-                                      third record buffer. */
+                                      take k_segsort, and segments longer than 64 records
+                                      (kSegMax) make the sort redo the kept input by the LSD
+                                      passes.  Needs a third record buffer. */
 #define LSB_OPT_EXCHANGE_GATHER 10 /* per-digit exchange forms with single-read local passes:
                                       1 (default) every exchange but the last only counts
                                       the next byte as the records arrive, and the next local
