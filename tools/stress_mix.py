@@ -78,6 +78,10 @@ def main():
     ap.add_argument("--max-log2", type=int, default=27)
     ap.add_argument("--trace", action="store_true", help="print each configuration before its sort")
     ap.add_argument("--stop-on-error", action="store_true", help="end at the first wrong sort or error")
+    ap.add_argument("--host-share", type=float, default=1 / 3,
+                    help="share of iterations that sort host-made (thinned / crowded) keys")
+    ap.add_argument("--hybrid", type=int, choices=(0, 1, 2), default=None,
+                    help="force LSB_OPT_HYBRID instead of drawing it (the draw still happens)")
     a = ap.parse_args()
     rng = random.Random(a.seed)
     t_end = time.time() + a.seconds
@@ -90,7 +94,9 @@ def main():
         split = rng.choice((0, 1, 2))
         hybrid = rng.choice((0, 1, 1, 2))
         gather = rng.choice((0, 1, 1))  # LSB_OPT_EXCHANGE_GATHER (per-digit exchange forms)
-        host = rng.random() < 1 / 3
+        if a.hybrid is not None:
+            hybrid = a.hybrid
+        host = rng.random() < a.host_share
         if host:
             n = min(n, 1 << 22)
             dist = "crowded" if rng.random() < 0.25 else "thinned"
