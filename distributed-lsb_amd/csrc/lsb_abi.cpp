@@ -92,7 +92,8 @@ int lsb_rank_footprint(int64_t n_total, int num_ranks, int radix_bits, int with_
     const int64_t cap_rec = rec_bytes((size_t)cap);  // a candidate holds as many records as A
     double share = 0.0;
     const int K = placement_request((double)cap_rec, &share);
-    *probe_bytes = K > 2 && cap_rec >= ((int64_t)1 << 30) ? (K - 2) * cap_rec : 0;
+    // One candidate beyond A and B is live at a time (alloc_records).
+    *probe_bytes = K > 2 && cap_rec >= ((int64_t)1 << 30) ? cap_rec : 0;
   }
   return LSB_OK;
 }
@@ -197,13 +198,21 @@ void lsb_destroy(lsb_ctx_t* c) {
 #endif
   // Every rank's streams first: a loopback rank's stream reads the other
   // ranks' buffers (exchange copies), and VMM record buffers are unmapped
-  // without the implicit device synchronisation hipFree has.
+  // without the implicit device synchronisation hipFree has.  (Debug builds
+  // check it, and LSB_TEARDOWN_LEGACY there restores the old order, one rank's
+  // own stream at a time, to show the check firing: free_rank.)
+#ifdef LSB_DEBUG
+  const bool legacy = getenv("LSB_TEARDOWN_LEGACY") != nullptr;
+#else
+  const bool legacy = false;
+#endif
   for (Rank& r : c->ranks) {
+    if (legacy) break;
     (void)hipSetDevice(r.dev);
     if (r.stream) (void)hipStreamSynchronize(r.stream);
     if (r.pstream) (void)hipStreamSynchronize(r.pstream);
   }
-  for (Rank& r : c->ranks) free_rank(r);
+  for (Rank& r : c->ranks) free_rank(r, c);
   for (auto& e : c->event_pool) (void)hipEventDestroy(e.second);
   if (c->comm) (void)ncclCommDestroy(c->comm);
   delete c;

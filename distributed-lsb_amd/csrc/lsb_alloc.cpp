@@ -134,9 +134,22 @@ int rec_alloc_group(const lsb_ctx* c, Elem** const* outs, int k, size_t count) {
     a.flags = hipMemAccessFlagsProtReadWrite;
     acc.push_back(a);
   }
-  for (int i = 0; i < k && e == hipSuccess; ++i) {
-    e = hipMemSetAccess(b[i].base, bytes, acc.data(), acc.size());
-    if (e != hipSuccess && acc.size() > 1) e = hipMemSetAccess(b[i].base, bytes, acc.data(), 1);  // owner only
+  for (int i = 0; i < k && e == hipSuccess; ++i) e = hipMemSetAccess(b[i].base, bytes, acc.data(), acc.size());
+  if (e != hipSuccess && acc.size() > 1) {
+    // The other devices of a loopback context cannot map the pieces: an
+    // owner-only mapping would fault at sort time on their copies and peer
+    // stores, so these buffers are hipMalloc'd instead, which peer access
+    // reaches (advisor r05).
+    for (VmmBuffer& x : b) vmm_release(x, piece);
+    (void)hipGetLastError();
+    for (int i = 0; i < k; ++i) {
+      const int rc = dev_alloc(outs[i], count);
+      if (rc != LSB_OK) {
+        for (int q = 0; q < i; ++q) (void)hipFree(*outs[q]);
+        return rc;
+      }
+    }
+    return LSB_OK;
   }
   if (e != hipSuccess) {
     const std::string why = hipGetErrorString(e);
@@ -206,7 +219,8 @@ int placement_candidates(double bytes, int cap) {
   int K = std::min(placement_request(bytes, &share), cap);
   size_t free_b = 0, total_b = 0;
   if (K > 2 && bytes >= (double)(1ull << 30) && hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
-    while (K > 2 && K * bytes > share * (double)free_b) --K;
+    // At most three candidates are live at once (alloc_records, alloc_third).
+    if (3 * bytes > share * (double)free_b) K = 2;
   } else {
     (void)hipGetLastError();
     K = 2;
@@ -312,6 +326,16 @@ int64_t record_capacity(int64_t per, int P) {
   return cap > 0 ? std::max(per, lsb::region_stride(cap) * lsb::kRegions) : per;
 }
 
+// The probe times each candidate once, as a destination: a buffer of pieces
+// is slow or fast as the destination of the LSD write pattern as a whole,
+// whatever the source (tools/kbench/pairbw2.hip), so the
+// round-5 matrix of K(K - 1) ordered pairs measured the same thing K - 1
+// times.  X (PCG keys) and Y come first, each timed as the other's
+// destination; every further candidate Z is timed as the destination of the
+// buffer holding the latest records, and whichever of the two kept buffers is
+// the slower destination is freed at once (or Z, if it is slower than both).
+// K timed passes (and one warm-up), and at most three buffers live: the
+// probe's transient memory is one buffer (round 5: K - 2 at once).
 int alloc_records(lsb_ctx* c, Rank& r) {
   const size_t per = (size_t)record_capacity(c->per, c->P);
   r.cap = (int64_t)per;
@@ -325,72 +349,69 @@ int alloc_records(lsb_ctx* c, Rank& r) {
     return rec_alloc_group(c, outs, early && atoi(early) ? 3 : 2, per);
   }
   std::vector<Elem*> cand;
-  LSB_TRY(alloc_candidates(c, per, K, 2, cand));
-  K = (int)cand.size();
+  LSB_TRY(alloc_candidates(c, per, 2, 2, cand));
+  Elem* keep[2] = {cand[0], cand[1]};
+  Elem* z = nullptr;
   auto give_up = [&](int rc) {
-    for (Elem* p : cand) rec_free(p);
+    for (Elem* p : {keep[0], keep[1], z}) rec_free(p);
     return rc;
   };
   int rc = onesweep_ensure(r);
   if (rc != LSB_OK) return give_up(rc);
-  std::vector<double> ms((size_t)K * K, 0.0);
-  std::vector<int> sorted_by(K, -8);
+  // LSB_PLACEMENT_PICK=worst keeps the slowest destinations instead
+  // (experiments: tools/alloc_probe.py checks that the probe predicts the passes).
+  const char* pick = getenv("LSB_PLACEMENT_PICK");
+  const bool pick_worst = pick && strcmp(pick, "worst") == 0;
+  auto better = [&](double a, double b) { return pick_worst ? a > b : a < b; };
   Prober pr(r.stream, r.here);
-  for (int k = 0; k < K && pr.err == hipSuccess; ++k)
-    pr.err = lsb::launch_pcg_fill(cand[k], r.here, 0x5eed + (uint64_t)k, 0, lsb::KeyGen(), r.stream);
-  (void)time_pass(r, pr, cand[0], cand[1], 0, r.os_hist);  // warm-up
-  sorted_by[1] = 0;
-  for (int x = 0; x < K; ++x)
-    for (int y = 0; y < K; ++y) {
-      if (x == y) continue;
-      const int shift = (sorted_by[x] + 8) & 63;
-      ms[(size_t)x * K + y] = time_pass(r, pr, cand[x], cand[y], shift, r.os_hist);
-      sorted_by[y] = shift;
+  pr.err = lsb::launch_pcg_fill(keep[0], r.here, 0x5eed, 0, lsb::KeyGen(), r.stream);
+  (void)time_pass(r, pr, keep[0], keep[1], 0, r.os_hist);  // warm-up
+  double ms[2];
+  ms[1] = time_pass(r, pr, keep[0], keep[1], 0, r.os_hist);  // Y as destination
+  ms[0] = time_pass(r, pr, keep[1], keep[0], 8, r.os_hist);  // X as destination (Y is ordered by byte 0)
+  const double first_pair = 0.5 * (ms[0] + ms[1]);
+  double worst = std::max(ms[0], ms[1]);
+  int src = 0, shift = 16;  // keep[src] holds the latest records, ordered by byte shift - 8
+  int tried = 2;
+  for (; tried < K && pr.err == hipSuccess; ++tried) {
+    if (rec_alloc(c, &z, per) != LSB_OK) {  // fewer candidates than hoped
+      (void)hipGetLastError();
+      z = nullptr;
+      break;
     }
+    const double t = time_pass(r, pr, keep[src], z, shift, r.os_hist);
+    shift = (shift + 8) & 63;
+    worst = std::max(worst, t);
+    const int slow = better(ms[0], ms[1]) ? 1 : 0;
+    if (better(t, ms[slow])) {  // z replaces the slower kept buffer and holds the latest records
+      rec_free(keep[slow]);
+      keep[slow] = z;
+      ms[slow] = t;
+      src = slow;
+    } else {
+      rec_free(z);
+    }
+    z = nullptr;
+  }
   if (pr.err != hipSuccess) return give_up(fail(LSB_ERR_HIP, "alloc_records: placement probe", hipGetErrorString(pr.err)));
   rc = probe_check(r);
   if (rc != LSB_OK) return give_up(rc);
-  // LSB_PLACEMENT_PICK=worst keeps the slowest pair instead (experiments:
-  // tools/alloc_probe.py checks that the probe predicts the passes).
-  const char* pick = getenv("LSB_PLACEMENT_PICK");
-  const bool pick_worst = pick && strcmp(pick, "worst") == 0;
-  int bx = 0, by = 1, wx = 0, wy = 1;
-  double best = 1e300, worst = 0.0;
-  for (int x = 0; x < K; ++x)
-    for (int y = x + 1; y < K; ++y) {
-      const double pair = 0.5 * (ms[(size_t)x * K + y] + ms[(size_t)y * K + x]);
-      if (pair < best) {
-        best = pair;
-        bx = x;
-        by = y;
-      }
-      if (pair > worst) {
-        worst = pair;
-        wx = x;
-        wy = y;
-      }
-    }
-  if (pick_worst) {
-    bx = wx;
-    by = wy;
-  }
-  r.placement_k = K;
-  r.placement_ms[0] = pick_worst ? worst : best;
-  r.placement_ms[1] = 0.5 * (ms[1] + ms[(size_t)K]);  // the first two buffers allocated
-  r.placement_ms[2] = worst;
-  r.A = cand[bx];
-  r.B = cand[by];
-  for (Elem* p : cand)
-    if (p != r.A && p != r.B) rec_free(p);
+  r.placement_k = tried;
+  r.placement_ms[0] = 0.5 * (ms[0] + ms[1]);
+  r.placement_ms[1] = first_pair;  // the first two buffers allocated
+  r.placement_ms[2] = worst;       // the slowest destination timed
+  r.A = keep[0];
+  r.B = keep[1];
   return LSB_OK;
 }
 
 // The third record buffer R (receive buffer of the exchanges, the hybrid's
-// third pass buffer), placed like A and B: among up to 3 candidates, the one
-// whose timed passes to and from B (scratch whenever R is first needed:
-// before a hybrid sort, at an exchange before its placement) take least time.
-// A may hold records by then and is not touched; the probe counts into a
-// histogram of its own, since a sort may hold one in r.os_hist.
+// third pass buffer), placed like A and B: among up to 3 candidates, the
+// fastest destination of a timed pass out of B (scratch whenever R is first
+// needed: before a hybrid sort, at an exchange before its placement), each
+// loser freed at once (two buffers live at most).  A may hold records by then
+// and is not touched; the probe counts into a histogram of its own, since a
+// sort may hold one in r.os_hist.
 int alloc_third(lsb_ctx* c, Rank& r) {
   // As many records as A and B: the hybrid permutes the three buffers, and
   // the regional first pass writes into whichever one is B by then.
@@ -398,33 +419,37 @@ int alloc_third(lsb_ctx* c, Rank& r) {
   int K = r.placement_k > 0 ? placement_candidates((double)per * sizeof(Elem), 3) : 1;  // probed A and B only
   if (K <= 2) K = 1;
   if (K == 1 || !r.os_status) return rec_alloc(c, &r.R, per);
-  std::vector<Elem*> cand;
-  LSB_TRY(alloc_candidates(c, per, K, 1, cand));
-  K = (int)cand.size();
   uint32_t* hist = nullptr;
-  int rc = K > 1 ? dev_alloc(&hist, (size_t)lsb::kOnesweepSubs * lsb::kBuckets) : LSB_OK;
+  LSB_TRY(dev_alloc(&hist, (size_t)lsb::kOnesweepSubs * lsb::kBuckets));
   Prober pr(r.stream, r.here);
-  int bk = 0;
-  double best = 1e300;
-  for (int k = 0; k < K && K > 1 && rc == LSB_OK; ++k) {
-    if (pr.err == hipSuccess)
-      pr.err = lsb::launch_pcg_fill(cand[k], r.here, 0x5eed + 16 + (uint64_t)k, 0, lsb::KeyGen(), r.stream);
-    const double t = time_pass(r, pr, cand[k], r.B, 0, hist) + time_pass(r, pr, r.B, cand[k], 8, hist);
-    if (t < best) {
-      best = t;
-      bk = k;
+  pr.err = lsb::launch_pcg_fill(r.B, r.here, 0x5eed + 16, 0, lsb::KeyGen(), r.stream);
+  Elem* best = nullptr;
+  double best_ms = 1e300;
+  int rc = LSB_OK;
+  for (int k = 0; k < K && pr.err == hipSuccess; ++k) {
+    Elem* z = nullptr;
+    if (rec_alloc(c, &z, per) != LSB_OK) {  // fewer candidates than hoped
+      (void)hipGetLastError();
+      break;
+    }
+    const double t = time_pass(r, pr, r.B, z, 0, hist);
+    if (t < best_ms) {
+      rec_free(best);
+      best = z;
+      best_ms = t;
+    } else {
+      rec_free(z);
     }
   }
   (void)hipFree(hist);
-  if (rc == LSB_OK && pr.err != hipSuccess) rc = fail(LSB_ERR_HIP, "alloc_third: placement probe", hipGetErrorString(pr.err));
-  if (rc == LSB_OK && K > 1) rc = probe_check(r);
+  if (pr.err != hipSuccess) rc = fail(LSB_ERR_HIP, "alloc_third: placement probe", hipGetErrorString(pr.err));
+  if (rc == LSB_OK && !best) rc = fail(LSB_ERR_NOMEM, "alloc_third", "record buffer");
+  if (rc == LSB_OK) rc = probe_check(r);
   if (rc != LSB_OK) {
-    for (Elem* p : cand) rec_free(p);
+    rec_free(best);
     return rc;
   }
-  r.R = cand[bk];
-  for (Elem* p : cand)
-    if (p != r.R) rec_free(p);
+  r.R = best;
   return LSB_OK;
 }
 

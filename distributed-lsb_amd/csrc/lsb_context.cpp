@@ -120,10 +120,41 @@ int init_rank(lsb_ctx* c, Rank& r, int rank, int dev) {
   return LSB_OK;
 }
 
-void free_rank(Rank& r) {
+int teardown_check(const lsb_ctx* c, const Rank& freeing) {
+  int busy = 0;
+  for (const Rank& q : c->ranks) {
+    (void)hipSetDevice(q.dev);
+    const hipStream_t s[2] = {q.stream, q.pstream};
+    for (int k = 0; k < 2; ++k) {
+      if (!s[k]) continue;
+      const hipError_t e = hipStreamQuery(s[k]);
+      (void)hipGetLastError();
+      if (e == hipSuccess) continue;
+      ++busy;
+      fprintf(stderr, "[lsb] teardown check: rank %d's %s not idle (%s) as rank %d's record buffers are freed\n",
+              q.rank, k ? "placement stream" : "stream", hipGetErrorString(e), freeing.rank);
+    }
+  }
+  (void)hipSetDevice(freeing.dev);
+  return busy;
+}
+
+void free_rank(Rank& r, const lsb_ctx* c) {
   (void)hipSetDevice(r.dev);
+  // LSB_TEARDOWN_LEGACY (debug builds only): the order before round 5's fix,
+  // this rank's stream alone, so that teardown_check can be seen to fire.
+#ifdef LSB_DEBUG
+  const bool legacy = getenv("LSB_TEARDOWN_LEGACY") != nullptr;
+#else
+  const bool legacy = false;
+#endif
   if (r.stream) (void)hipStreamSynchronize(r.stream);
-  if (r.pstream) (void)hipStreamSynchronize(r.pstream);  // placements read R and write B
+  if (r.pstream && !legacy) (void)hipStreamSynchronize(r.pstream);  // placements read R and write B
+#ifdef LSB_DEBUG
+  if (c) (void)teardown_check(c, r);
+#else
+  (void)c;
+#endif
   for (void* p : r.ipc_opened) (void)hipIpcCloseMemHandle(p);
   (void)hipFree(r.peer_base);
   (void)hipFree(r.split_state);
@@ -209,11 +240,21 @@ int coll_allgather_u64(lsb_ctx* c, Rank& r, const uint64_t* send, uint64_t* recv
 // carrying part i of every peer's range on both sides.  (The reference's
 // MPI_Alltoallv takes int counts and cannot pass 2^31 records at all,
 // mpi/mpi_lsbsort.cpp:292-313.)
+size_t max_call_u64() {
+  static const size_t v = [] {
+    const char* e = getenv("LSB_RCCL_CALL_U64");
+    const long long x = e ? atoll(e) : 0;
+    return x > 0 ? (size_t)x : kMaxCallU64;
+  }();
+  return v;
+}
+
 int coll_alltoallv_u64(lsb_ctx* c, Rank& r, const uint64_t* send, const size_t* sc,
                        const size_t* sd, uint64_t* recv, const size_t* rc, const size_t* rd,
                        size_t bound) {
   const int P = c->P;
-  const size_t k = c->mode == Mode::kRccl ? std::max<size_t>(1, (bound + kMaxCallU64 - 1) / kMaxCallU64) : 1;
+  const size_t lim = max_call_u64();
+  const size_t k = c->mode == Mode::kRccl ? std::max<size_t>(1, (bound + lim - 1) / lim) : 1;
   if (k > 1) {
     std::vector<size_t> sc1(P), sd1(P), rc1(P), rd1(P);
     auto cut = [&](size_t n, size_t i) { return (size_t)((unsigned __int128)n * i / k); };

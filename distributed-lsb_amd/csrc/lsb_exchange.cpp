@@ -279,12 +279,14 @@ int peer_setup(lsb_ctx* c) {
   Rank& r = c->ranks[0];
   HIP_TRY(hipSetDevice(r.dev));
   // IPC handles name hipMalloc memory only: a record buffer built from VMM
-  // pieces (rec_alloc) is replaced by a hipMalloc'd one holding its records.
+  // pieces (rec_alloc) is replaced by a hipMalloc'd one holding its records,
+  // of the same capacity: a later sort with the exchange off may start with
+  // the regional first pass, which writes r.cap slots (advisor r05).
   for (int k = 0; k < 2; ++k) {
     Elem* old = r.buf[k];
     if (!rec_is_vmm(old)) continue;
     Elem* nu = nullptr;
-    LSB_TRY(dev_alloc(&nu, (size_t)c->per));
+    LSB_TRY(dev_alloc(&nu, (size_t)std::max(r.cap, c->per)));
     HIP_TRY(hipMemcpyAsync(nu, old, sizeof(Elem) * (size_t)c->per, hipMemcpyDeviceToDevice, r.stream));
     HIP_TRY(hipStreamSynchronize(r.stream));
     for (Elem** p : {&r.A, &r.B, &r.R})
@@ -414,7 +416,7 @@ int exchange_rccl(lsb_ctx* c, int digit) {
   // every rank: by the largest peer segment of this exchange on any rank, one
   // all-reduce of one word, asked only when a block could exceed it at all.
   int64_t seg = c->per;
-  if (c->mode == Mode::kRccl && (size_t)slice_bound(c->per, 0, slices_of(c)) * 2 > kMaxCallU64) {
+  if (c->mode == Mode::kRccl && (size_t)slice_bound(c->per, 0, slices_of(c)) * 2 > max_call_u64()) {
     int64_t m = 0;
     for (int q = 0; q < P; ++q)
       if (q != me || c->self_coll) m = std::max(m, std::max(r.send_counts[q], r.recv_counts[q]));

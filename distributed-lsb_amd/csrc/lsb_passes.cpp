@@ -206,8 +206,9 @@ std::vector<int> varying_bytes(uint64_t varying) {
 // the sub-array histogram of digits[0] over r.A.
 // From digits[from] on; rp: digits[from]'s pass reads the regional layout
 // (its input's histogram in os_hist[from & 1]).
+// *disarm (when given) turns false once pass `from` is queued.
 int onesweep_digits(lsb_ctx* c, Rank& r, const std::vector<int>& digits, int* passes, size_t from = 0,
-                    const lsb::RegionPass* rp = nullptr) {
+                    const lsb::RegionPass* rp = nullptr, bool* disarm = nullptr) {
   uint32_t* hist[2] = {r.os_hist, r.os_hist + lsb::kOnesweepSubs * lsb::kBuckets};
   for (size_t i = from; i < digits.size(); ++i) {
     const int shift = digits[i] * lsb::kDigitBits;
@@ -221,6 +222,7 @@ int onesweep_digits(lsb_ctx* c, Rank& r, const std::vector<int>& digits, int* pa
     }
     LSB_TRY(onesweep_launch(c, r, shift, next, hist[i & 1], hist[(i + 1) & 1], x));
     ++*passes;
+    if (disarm) *disarm = false;
   }
   return LSB_OK;
 }
@@ -282,9 +284,16 @@ int region_sample(lsb_ctx* c, Rank& r, int byte, bool* go, uint64_t* seen) {
   for (int b = 0; b < 64 / lsb::kDigitBits; ++b)
     every_byte = every_byte && ((*seen >> (b * lsb::kDigitBits)) & (lsb::kBuckets - 1)) != 0;
   // No bucket over the mean by more than max(10 %, 6 standard deviations of
-  // a uniform bucket's count in a sample this size).
-  const double mean = (double)S / lsb::kBuckets;
-  *go = every_byte && S > 0 && (double)top <= mean + std::max(0.1 * mean, 6.0 * std::sqrt(mean));
+  // a uniform bucket's count in a sample this size), nor by more than the
+  // regions' own slack (region_cap over the uniform mean: +1.6 % at 2^30)
+  // plus 4 standard deviations: at 2^30 a bucket 8-10 % over the mean would
+  // pass the first bound and overflow its regions for certain (advisor r05).
+  // Below ~5 % the sample cannot tell such a bucket from noise; the overflow
+  // word catches it.
+  const double mean = (double)S / lsb::kBuckets, sd = std::sqrt(mean);
+  const double slack = (double)r.rg_cap / (double)lsb::region_mean(r.here);
+  const double gate = std::min(mean + std::max(0.1 * mean, 6.0 * sd), mean * slack + 4.0 * sd);
+  *go = every_byte && S > 0 && (double)top <= gate;
   return LSB_OK;
 }
 
@@ -476,6 +485,13 @@ int LocalSort::begin() {
     if (region_applies(c, r)) LSB_TRY(region_sample(c, r, 0, &region, &varying));
     if (region) {  // every digit varies: no span read
       c->last_first = LSB_FIRST_REGIONAL;
+      // Armed until the pass that reads the regional layout is queued: A then
+      // holds the layout (gaps of stale slots, no permutation), so an error
+      // return before that restores the input to A (advisor r05).
+      X0 = r.A;
+      X1 = r.B;
+      X2 = r.R;
+      armed = true;
       return region_first(c, r, 0, lsb::kDigitBits, &passes);
     }
     varying = ~0ull;
@@ -529,7 +545,7 @@ int LocalSort::queue() {
     if (r.rg_h[kRgOvf] == 0) {
       r.os_halves = 1;
       const lsb::RegionPass rp = region_pass(r);
-      LSB_TRY(onesweep_digits(c, r, digits, &passes, 1, &rp));
+      LSB_TRY(onesweep_digits(c, r, digits, &passes, 1, &rp, &armed));
       kind = kDone;
       return queue_err_word();
     }
@@ -537,6 +553,7 @@ int LocalSort::queue() {
     // read it and wrote the other buffer), with the usual first read.
     c->last_first = LSB_FIRST_REGIONAL_REDONE;
     std::swap(r.A, r.B);
+    armed = false;
     passes = 0;
     c->pass_cursor = 0;
     c->cur_pass = 0;

@@ -307,7 +307,13 @@ int placement_request(double bytes, double* free_share);
 int alloc_records(lsb_ctx* c, Rank& r);  // A and B (placement-calibrated)
 int alloc_third(lsb_ctx* c, Rank& r);    // R, placed against A and B
 int init_rank(lsb_ctx* c, Rank& r, int rank, int dev);
-void free_rank(Rank& r);
+// Frees r's buffers once r's streams are idle.  c (LSB_DEBUG builds): check
+// first that every rank's streams of c are idle (teardown_check).
+void free_rank(Rank& r, const lsb_ctx* c = nullptr);
+// Debug builds: every rank's stream and placement stream must be idle before
+// any record buffer of the context is unmapped (VMM unmapping does not wait
+// for the device).  Reports each busy stream on stderr; returns how many.
+int teardown_check(const lsb_ctx* c, const Rank& freeing);
 Rank* local_rank(lsb_ctx* c, int rank);
 int check_ctx(const lsb_ctx* c);
 lsb_ctx* new_ctx(int64_t n_total, int num_ranks, int radix_bits);
@@ -317,6 +323,9 @@ int ops_fail(const char* what);
 int coll_allgather_u64(lsb_ctx* c, Rank& r, const uint64_t* send, uint64_t* recv, size_t count);
 // RCCL calls carry at most this many u64 (1 GiB) per peer (coll_alltoallv_u64).
 constexpr size_t kMaxCallU64 = (size_t)1 << 27;
+// The bound in force: kMaxCallU64, or LSB_RCCL_CALL_U64 (tests: a small bound
+// makes small multi-rank sorts take the cut path, advisor r05).
+size_t max_call_u64();
 int coll_alltoallv_u64(lsb_ctx* c, Rank& r, const uint64_t* send, const size_t* sc,
                        const size_t* sd, uint64_t* recv, const size_t* rc, const size_t* rd,
                        size_t bound);

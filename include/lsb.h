@@ -338,14 +338,16 @@ int  lsb_get_pass_exchange(lsb_ctx_t* ctx, int pass, int64_t* bytes, double* wir
  * LSB_RECORD_ALLOC=malloc: hipMalloc).  Such a buffer can still be a slow
  * pass destination as a whole, so a rank whose buffers hold
  * >= 4 GiB and that shares its device with no other rank of the context
- * allocates 4 candidate buffers (LSB_PLACEMENT_CANDIDATES = K: K of them, at
- * most 8, for buffers of >= 1 GiB; 0: none), as many as fit in half the
- * free memory (90 % when K is set; a transient peak of K record buffers,
- * see lsb_rank_footprint), times one k_onesweep pass over uniform keys
- * between every ordered pair, keeps the pair fastest both ways and frees
- * the rest.  candidates = 0: no probe ran.  Milliseconds per pass, mean of both directions: the chosen
- * pair, the first two buffers allocated (what a plain allocation would have
- * kept) and the slowest pair. */
+ * tries 4 candidate buffers (LSB_PLACEMENT_CANDIDATES = K: K of them, at
+ * most 8, for buffers of >= 1 GiB; 0: none) when three fit in half the free
+ * memory (90 % when K is set).  Each candidate is timed once as the
+ * destination of one k_onesweep pass over uniform keys (the speed that
+ * differs); the two fastest destinations are kept and every other candidate
+ * is freed as soon as it loses, so the probe holds at most one record buffer
+ * more than A and B (see lsb_rank_footprint).  candidates = the candidates
+ * timed, 0: no probe ran.  Milliseconds per pass as a destination: the mean
+ * of the chosen two, the mean of the first two allocated (what a plain
+ * allocation would have kept) and the slowest candidate. */
 int  lsb_get_placement(lsb_ctx_t* ctx, int rank, int* candidates, double* chosen_ms,
                        double* first_pair_ms, double* worst_ms);
 
@@ -358,7 +360,8 @@ int  lsb_get_placement(lsb_ctx_t* ctx, int rank, int* candidates, double* chosen
  * per 4096-record tile), the gathered passes' tile descriptors (exchanges),
  * and the count and plan tables.  *probe_bytes: what the placement probe
  * (by default 4 candidates for buffers of >= 4 GiB; LSB_PLACEMENT_CANDIDATES,
- * read from the environment now) holds on top while it runs, at most (a rank
+ * read from the environment now) holds on top while it runs, at most: one
+ * record buffer (a rank
  * that shares its device with another rank of its context runs none); 0 when
  * no probe would run.  A model of
  * init_rank's allocations, checked against the device's own free-memory

@@ -343,8 +343,9 @@ def test_rank_footprint_model(lsb_built, monkeypatch):
     """lsb_rank_footprint (host arithmetic): record buffers rounded up to whole
     1 GiB VMM pieces (hipMalloc'd ones are not), R only with an exchange or
     the hybrid, 4 B of look-back row per bucket per 4096-record tile, and the
-    placement probe's K - 2 extra candidates (by default 4 candidates for
-    buffers of at least 4 GiB; LSB_PLACEMENT_CANDIDATES = K sets K)."""
+    placement probe's one extra candidate live at a time (by default 4
+    candidates for buffers of at least 4 GiB; LSB_PLACEMENT_CANDIDATES = K
+    sets K; round 6: K passes, losers freed at once)."""
     L = lsb_built
     gib = 1 << 30
     monkeypatch.delenv("LSB_PLACEMENT_CANDIDATES", raising=False)
@@ -359,10 +360,10 @@ def test_rank_footprint_model(lsb_built, monkeypatch):
     slots = 2048 * 130 * 4096
     f = L.rank_footprint(n, 1, 8)
     assert 0 <= f["bytes"] - 34 * gib - rows - (slots // 4096) * 256 * 4 < 64 << 20
-    assert f["probe_bytes"] == 2 * 17 * gib  # the default probe: 4 candidates of 17 pieces
+    assert f["probe_bytes"] == 17 * gib  # the default probe: one candidate of 17 pieces beside A and B
     monkeypatch.setenv("LSB_REGION_MIN", str(1 << 40))  # no regional slots from here on
     f = L.rank_footprint(n, 1, 8)
-    assert f["probe_bytes"] == 2 * 16 * gib and 0 <= f["bytes"] - 32 * gib - rows < 64 << 20
+    assert f["probe_bytes"] == 16 * gib and 0 <= f["bytes"] - 32 * gib - rows < 64 << 20
     assert L.rank_footprint(n // 8, 1, 8)["probe_bytes"] == 0  # 2 GiB buffers: no default probe
     extra = L.rank_footprint(n, 1, 8, with_recv=True)["bytes"] - f["bytes"]
     assert 16 * gib <= extra < 16 * gib + (64 << 20)  # R, and the gathered passes' tile descriptors
@@ -374,7 +375,7 @@ def test_rank_footprint_model(lsb_built, monkeypatch):
     monkeypatch.setenv("LSB_PLACEMENT_CANDIDATES", "0")
     assert L.rank_footprint(n, 1, 8)["probe_bytes"] == 0
     monkeypatch.setenv("LSB_PLACEMENT_CANDIDATES", "8")
-    assert L.rank_footprint(n, 1, 8)["probe_bytes"] == 6 * 16 * gib
+    assert L.rank_footprint(n, 1, 8)["probe_bytes"] == 16 * gib  # 8 candidates, still one at a time
     assert L.rank_footprint(1 << 20, 1, 8)["probe_bytes"] == 0  # buffers under 1 GiB: no probe
     # P ranks: per = ceil(n / P) records each
     assert L.rank_footprint(8 * n, 8, 16, with_recv=True)["bytes"] > 48 * gib

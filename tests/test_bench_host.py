@@ -220,5 +220,5 @@ def test_eight_rank_memory_fits_the_device(candidates):
     m = out["device_memory"]
     gib = 1 << 30
     assert 48 * gib <= m["bytes"] < 49 * gib  # A, B, R of 16 GiB each + 1/64 look-back rows
-    assert m["probe_bytes"] == (6 if candidates else 2) * 16 * gib
+    assert m["probe_bytes"] == 16 * gib  # one candidate beside A and B at a time, whatever K
     assert m["device_bytes"] == 288 * 10**9 and m["fits"] and m["peak_frac"] < 0.9

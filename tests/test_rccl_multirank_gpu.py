@@ -103,3 +103,24 @@ def test_real_rccl_ranks_two_gib_segments(lsb_built):
     assert all(r["verify"]) and all(r["check_sorted"]), r
     assert all(b >= (1 << 31) for b in r["rccl_bytes"]), r  # >= 2 GiB handed to RCCL per rank
     assert rc == 0
+
+
+@pytest.mark.parametrize("bits,n,world,exchange", [
+    (16, 1_000_000, 2, "alltoallv"),
+    (16, 1_048_576, 8, "p2p"),
+    (64, 1_000_003, 4, "alltoallv"),
+])
+def test_real_rccl_ranks_cut_calls(lsb_built, bits, n, world, exchange):
+    """The cut of RCCL calls between real ranks (advisor r05): with the per-peer
+    call bound lowered to 4096 u64 (LSB_RCCL_CALL_U64; 2^27 by default) every
+    slice goes as several calls, and at P > 1 the per-digit exchange agrees on
+    the cut through its all-reduce of the largest peer segment.  The golden
+    digest, every rank verified, and no call above the bound."""
+    bound = 4096
+    rc, r = _run(bits, n, world, exchange, env={"LSB_RCCL_CALL_U64": str(bound)})
+    assert r["status"] == "ok", r
+    assert r["golden_match"] is True, r
+    assert all(r["verify"]) and all(r["check_sorted"]), r
+    assert all(b > 0 for b in r["rccl_bytes"]), r
+    assert all(m <= world * bound * 8 for m in r["rccl_max_call_bytes"]), r
+    assert rc == 0
