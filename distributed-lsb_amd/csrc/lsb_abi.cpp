@@ -211,6 +211,7 @@ void lsb_destroy(lsb_ctx_t* c) {
     (void)hipSetDevice(r.dev);
     if (r.stream) (void)hipStreamSynchronize(r.stream);
     if (r.pstream) (void)hipStreamSynchronize(r.pstream);
+    if (r.xstream) (void)hipStreamSynchronize(r.xstream);
   }
   for (Rank& r : c->ranks) free_rank(r, c);
   for (auto& e : c->event_pool) (void)hipEventDestroy(e.second);
@@ -259,6 +260,11 @@ int lsb_set_option(lsb_ctx_t* c, int option, int64_t value) {
     case LSB_OPT_ONESWEEP_SPLIT:
       if (value < 0 || value > 2) return fail(LSB_ERR_INVALID, "lsb_set_option", "split must be 0..2");
       c->os_split = (int)value;
+      return LSB_OK;
+    case LSB_OPT_EXCHANGE_CHUNKS:
+      if (value != 0 && value != 2 && value != 4 && value != 8)
+        return fail(LSB_ERR_INVALID, "lsb_set_option", "exchange chunks must be 0, 2, 4 or 8");
+      c->xchunks = (int)value;
       return LSB_OK;
     case LSB_OPT_EXCHANGE_SLICES:
       if (value < 1 || value > 64)

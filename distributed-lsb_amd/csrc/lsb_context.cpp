@@ -124,15 +124,16 @@ int teardown_check(const lsb_ctx* c, const Rank& freeing) {
   int busy = 0;
   for (const Rank& q : c->ranks) {
     (void)hipSetDevice(q.dev);
-    const hipStream_t s[2] = {q.stream, q.pstream};
-    for (int k = 0; k < 2; ++k) {
+    const hipStream_t s[3] = {q.stream, q.pstream, q.xstream};
+    const char* name[3] = {"stream", "placement stream", "wire stream"};
+    for (int k = 0; k < 3; ++k) {
       if (!s[k]) continue;
       const hipError_t e = hipStreamQuery(s[k]);
       (void)hipGetLastError();
       if (e == hipSuccess) continue;
       ++busy;
       fprintf(stderr, "[lsb] teardown check: rank %d's %s not idle (%s) as rank %d's record buffers are freed\n",
-              q.rank, k ? "placement stream" : "stream", hipGetErrorString(e), freeing.rank);
+              q.rank, name[k], hipGetErrorString(e), freeing.rank);
     }
   }
   (void)hipSetDevice(freeing.dev);
@@ -150,6 +151,7 @@ void free_rank(Rank& r, const lsb_ctx* c) {
 #endif
   if (r.stream) (void)hipStreamSynchronize(r.stream);
   if (r.pstream && !legacy) (void)hipStreamSynchronize(r.pstream);  // placements read R and write B
+  if (r.xstream && !legacy) (void)hipStreamSynchronize(r.xstream);  // the chunked exchange's wire
 #ifdef LSB_DEBUG
   if (c) (void)teardown_check(c, r);
 #else
@@ -171,6 +173,19 @@ void free_rank(Rank& r, const lsb_ctx* c) {
   (void)hipHostFree(r.rg_h);
   (void)hipFree(r.gstart);
   (void)hipFree(r.gdesc);
+  (void)hipFree(r.ck_hist);
+  (void)hipFree(r.ck_counts);
+  (void)hipHostFree(r.ck_counts_h);
+  (void)hipHostFree(r.lo_hist_h);
+  if (r.xstream) {
+    (void)hipStreamSynchronize(r.xstream);
+    (void)hipStreamDestroy(r.xstream);
+  }
+  for (hipEvent_t e : r.ck_hi)
+    if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : r.ck_wire)
+    if (e) (void)hipEventDestroy(e);
+  if (r.xdone) (void)hipEventDestroy(r.xdone);
   (void)hipFree(r.seg_base);
   (void)hipFree(r.os_hist);
   (void)hipFree(r.os_ctr);
@@ -251,8 +266,9 @@ size_t max_call_u64() {
 
 int coll_alltoallv_u64(lsb_ctx* c, Rank& r, const uint64_t* send, const size_t* sc,
                        const size_t* sd, uint64_t* recv, const size_t* rc, const size_t* rd,
-                       size_t bound) {
+                       size_t bound, hipStream_t stream) {
   const int P = c->P;
+  hipStream_t st = stream ? stream : r.stream;
   const size_t lim = max_call_u64();
   const size_t k = c->mode == Mode::kRccl ? std::max<size_t>(1, (bound + lim - 1) / lim) : 1;
   if (k > 1) {
@@ -265,7 +281,7 @@ int coll_alltoallv_u64(lsb_ctx* c, Rank& r, const uint64_t* send, const size_t* 
         rd1[q] = rd[q] + cut(rc[q], i);
         rc1[q] = cut(rc[q], i + 1) - cut(rc[q], i);
       }
-      LSB_TRY(coll_alltoallv_u64(c, r, send, sc1.data(), sd1.data(), recv, rc1.data(), rd1.data(), 0));
+      LSB_TRY(coll_alltoallv_u64(c, r, send, sc1.data(), sd1.data(), recv, rc1.data(), rd1.data(), 0, st));
     }
     return LSB_OK;
   }
@@ -282,12 +298,12 @@ int coll_alltoallv_u64(lsb_ctx* c, Rank& r, const uint64_t* send, const size_t* 
   if (c->cur_pass >= 0 && c->cur_pass < LSB_MAX_PASSES) c->pass_xbytes[c->cur_pass] += call_bytes;
   if (c->mode == Mode::kRccl) {
     if (!c->p2p) {
-      RCCL_TRY(ncclAllToAllv(send, sc, sd, recv, rc, rd, ncclUint64, c->comm, r.stream));
+      RCCL_TRY(ncclAllToAllv(send, sc, sd, recv, rc, rd, ncclUint64, c->comm, st));
     } else {  // the same exchange as explicit grouped point-to-point calls
       RCCL_TRY(ncclGroupStart());
       for (int q = 0; q < P; ++q) {
-        if (sc[q] > 0) RCCL_TRY(ncclSend(send + sd[q], sc[q], ncclUint64, q, c->comm, r.stream));
-        if (rc[q] > 0) RCCL_TRY(ncclRecv(recv + rd[q], rc[q], ncclUint64, q, c->comm, r.stream));
+        if (sc[q] > 0) RCCL_TRY(ncclSend(send + sd[q], sc[q], ncclUint64, q, c->comm, st));
+        if (rc[q] > 0) RCCL_TRY(ncclRecv(recv + rd[q], rc[q], ncclUint64, q, c->comm, st));
       }
       RCCL_TRY(ncclGroupEnd());
     }
@@ -337,6 +353,14 @@ lsb_ctx* new_ctx(int64_t n_total, int num_ranks, int radix_bits) {
   // LSB_REGION_FIRST=0: contexts start with the option off (A/B runs of
   // programs that do not set options, e.g. bench.py).
   if (const char* e = getenv("LSB_REGION_FIRST")) c->region = atoi(e) != 0;
+  // LSB_EXCHANGE_CHUNKS=C: contexts start with LSB_OPT_EXCHANGE_CHUNKS = C
+  // (A/B runs of programs that do not set options); LSB_XCHUNK_RESERVE: the
+  // chunk passes' grid leaves that many workgroups to the wire (experiments).
+  if (const char* e = getenv("LSB_EXCHANGE_CHUNKS")) {
+    const int v = atoi(e);
+    c->xchunks = v == 2 || v == 4 || v == 8 ? v : 0;
+  }
+  if (const char* e = getenv("LSB_XCHUNK_RESERVE")) c->xchunk_reserve = std::max(0, atoi(e));
   return c;
 }
 

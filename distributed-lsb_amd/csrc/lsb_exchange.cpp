@@ -144,7 +144,8 @@ int place_self(lsb_ctx* c, Rank& r, int shift) {
     lsb::GatherSrc& g = r.gsrc;
     g.R = r.R;
     g.A = r.A;
-    g.self_adj = r.send_displs[me] - r.recv_displs[me];
+    for (int64_t& a : g.self_adj) a = r.send_displs[me] - r.recv_displs[me];
+    g.chunk_shift = 8;
     g.place = r.place;
     g.gstart = r.gstart;
     g.gadj = r.gstart + (size_t)c->P * c->nb;
@@ -461,6 +462,337 @@ int exchange_digit(lsb_ctx* c, int digit) {
   return exchange_loopback(c, digit);
 }
 
+// ---- the per-digit exchange in chunks (LSB_OPT_EXCHANGE_CHUNKS) -------------
+// the exchange of chunk k overlaps the local
+// work of chunk k + 1.  The reference runs localShuffle to the end and only
+// then the whole exchange (mpi/mpi_lsbsort.cpp:481-577), and so does
+// exchange_digit: the high-byte pass, then the wire.  Here, for a 16-bit
+// digit d whose low-byte pass has run (A sorted by the low byte l):
+//   1. one read of A (launch_count16_chunks) counts the digit's 65536 values
+//      and, per chunk k (the records with l in [k 256 / C, (k + 1) 256 / C):
+//      a contiguous range of A), the high byte's sub-array histogram;
+//   2. the counts are all-gathered and planned as before, except that a
+//      source's pieces lie in R in chunk order (launch_plan with cshift);
+//   3. chunk by chunk: chunk k's high-byte pass (one k_onesweep over its range
+//      of A, into the same range of B) on the rank's stream, then chunk k's
+//      all-to-all on the wire stream while chunk k + 1's pass runs, then its
+//      count-only placement (or, the last exchange, its placement once every
+//      pass is done) on the placement stream.
+// Inside chunk k the records end up ordered by (h, l), so every owner's
+// share is one contiguous range, and a digit's records all lie in one chunk:
+// the placed order, (digit, source), is the reference's, and the output is
+// the same bit for bit.  The price is step 1's read (16 B per record); what it
+// buys is the high-byte pass under the wire.
+constexpr int64_t kChunkMinPer = int64_t(1) << 16;
+
+bool chunked_applies(const lsb_ctx* c, uint64_t varying, int digit) {
+  if (c->xchunks < 2 || c->bits != 16 || c->peer || c->mode == Mode::kOps || !exchanging(c)) return false;
+  const int lo = digit * 16;
+  if (((varying >> lo) & 0xFF) == 0 || ((varying >> (lo + 8)) & 0xFF) == 0) return false;
+  return c->per >= kChunkMinPer;
+}
+
+namespace {
+
+int cshift_of(int C) { return C >= 8 ? 5 : C == 4 ? 6 : 7; }
+
+// One rank's chunk geometry (host) after the plan.
+struct ChunkGeom {
+  std::vector<int64_t> lo;     // [C + 1] chunk bounds in A and B
+  std::vector<int64_t> send;   // [q * C + k] my records of chunk k for owner q
+  std::vector<int64_t> recv;   // [s * C + k] source s's records of chunk k for me
+  std::vector<int64_t> sdisp;  // [q * C + k] where owner q's share starts inside chunk k
+  std::vector<int64_t> rpre;   // [s * C + k] where chunk k starts inside source s's range of R
+};
+
+int chunk_ensure(lsb_ctx* c, Rank& r) {
+  if (r.xstream) return LSB_OK;
+  HIP_TRY(hipSetDevice(r.dev));
+  if (!r.ck_hist) LSB_TRY(dev_alloc(&r.ck_hist, (size_t)lsb::kMaxExchangeChunks * lsb::kOnesweepSubs * lsb::kBuckets));
+  if (!r.ck_counts) LSB_TRY(dev_alloc(&r.ck_counts, (size_t)2 * c->P * lsb::kMaxExchangeChunks));
+  if (!r.ck_counts_h) LSB_TRY(host_alloc(&r.ck_counts_h, (size_t)2 * c->P * lsb::kMaxExchangeChunks));
+  if (!r.lo_hist_h) LSB_TRY(host_alloc(&r.lo_hist_h, (size_t)lsb::kOnesweepSubs * lsb::kBuckets));
+  for (hipEvent_t& e : r.ck_hi)
+    if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  for (hipEvent_t& e : r.ck_wire)
+    if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  if (!r.xdone) HIP_TRY(hipEventCreateWithFlags(&r.xdone, hipEventDisableTiming));
+  HIP_TRY(hipStreamCreateWithFlags(&r.xstream, hipStreamNonBlocking));  // last: marks the set complete
+  return LSB_OK;
+}
+
+// The plan in chunk order; the send / recv totals and the per-chunk counts
+// come back to the host (after a stream sync: chunk_geom).
+int chunk_plan(lsb_ctx* c, Rank& r, int cs) {
+  HIP_TRY(hipSetDevice(r.dev));
+  if (r.gather_next && !r.gstart) {
+    LSB_TRY(dev_alloc(&r.gstart, (size_t)2 * c->P * c->nb));  // gstart, then gadj
+    LSB_TRY(dev_alloc(&r.gdesc, (size_t)lsb::onesweep_tiles(r.here)));
+  }
+  const int C = lsb::kBuckets >> cs;
+  {
+    Timer t(c, &r, LSB_K_EXCHANGE);
+    HIP_TRY(lsb::launch_plan(r.gather, c->P, c->nb, r.rank, c->n, r.plan_work, r.plan_total, r.place,
+                             r.plan_counts, r.stream, r.gather_next ? r.gstart : nullptr, cs, r.ck_counts));
+  }
+  HIP_TRY(hipMemcpyAsync(r.counts_h, r.plan_counts, sizeof(int64_t) * 2 * c->P, hipMemcpyDeviceToHost, r.stream));
+  HIP_TRY(hipMemcpyAsync(r.ck_counts_h, r.ck_counts, sizeof(int64_t) * 2 * c->P * C, hipMemcpyDeviceToHost,
+                         r.stream));
+  return LSB_OK;
+}
+
+int chunk_geom(lsb_ctx* c, Rank& r, int C, ChunkGeom& g) {
+  const int P = c->P, lw = lsb::kBuckets / C;
+  g.lo.assign(C + 1, 0);
+  if (r.here > 0) {
+    int64_t acc = 0;
+    for (int l = 0; l < lsb::kBuckets; ++l) {
+      if (l % lw == 0) g.lo[l / lw] = acc;
+      for (int x = 0; x < lsb::kOnesweepSubs; ++x) acc += r.lo_hist_h[x * lsb::kBuckets + l];
+    }
+    g.lo[C] = acc;
+    if (acc != r.here) return fail(LSB_ERR_STATE, "exchange_chunked", "chunk bounds do not cover the block");
+  }
+  g.send.assign((size_t)P * C, 0);
+  g.recv.assign((size_t)P * C, 0);
+  g.sdisp.assign((size_t)P * C, 0);
+  g.rpre.assign((size_t)P * C, 0);
+  for (int i = 0; i < P * C; ++i) {
+    g.send[i] = r.ck_counts_h[i];
+    g.recv[i] = r.ck_counts_h[(size_t)P * C + i];
+  }
+  for (int k = 0; k < C; ++k) {
+    int64_t a = 0;
+    for (int q = 0; q < P; ++q) {
+      g.sdisp[(size_t)q * C + k] = a;
+      a += g.send[(size_t)q * C + k];
+    }
+    if (a != g.lo[k + 1] - g.lo[k]) return fail(LSB_ERR_STATE, "exchange_chunked", "chunk send counts");
+  }
+  for (int q = 0; q < P; ++q) {
+    int64_t a = 0, sa = 0;
+    for (int k = 0; k < C; ++k) {
+      g.rpre[(size_t)q * C + k] = a;
+      a += g.recv[(size_t)q * C + k];
+      sa += g.send[(size_t)q * C + k];
+    }
+    if (a != r.recv_counts[q] || sa != r.send_counts[q])
+      return fail(LSB_ERR_STATE, "exchange_chunked", "chunk counts do not add up");
+  }
+  return LSB_OK;
+}
+
+}  // namespace
+
+int exchange_chunked(lsb_ctx* c, int digit, const std::vector<const uint32_t*>& lo_hist) {
+  ++c->xs_exchanges;
+  const int C = std::min(c->xchunks, lsb::kMaxExchangeChunks), cs = cshift_of(C), P = c->P;
+  const size_t nb = (size_t)c->nb;
+  const int shift = digit * 16, hi_shift = shift + lsb::kDigitBits;
+  const bool loop = c->mode == Mode::kLoopback;
+  const size_t nr = c->ranks.size();
+  std::vector<ChunkGeom> geo(nr);
+  std::vector<Elem*> X(nr), Y(nr);  // the high-byte pass reads X (A, sorted by l) and writes Y (B)
+  // 1. the count read
+  for (size_t i = 0; i < nr; ++i) {
+    Rank& r = c->ranks[i];
+    LSB_TRY(chunk_ensure(c, r));
+    LSB_TRY(ensure_recv(c, r));
+    HIP_TRY(hipSetDevice(r.dev));
+    X[i] = r.A;
+    Y[i] = r.B;
+    {
+      Timer t(c, &r, LSB_K_UPSWEEP);
+      HIP_TRY(lsb::launch_count16_chunks(r.A, r.here, shift, lo_hist[i], cs, r.os_grid, r.totals16, r.ck_hist,
+                                         r.stream));
+    }
+    HIP_TRY(hipMemcpyAsync(r.lo_hist_h, lo_hist[i], sizeof(uint32_t) * lsb::kOnesweepSubs * lsb::kBuckets,
+                           hipMemcpyDeviceToHost, r.stream));
+  }
+  // 2. the counts to every rank, the plan in chunk order
+  if (loop) {
+    for (Rank& r : c->ranks) {
+      HIP_TRY(hipSetDevice(r.dev));
+      HIP_TRY(hipStreamSynchronize(r.stream));
+    }
+    for (Rank& q : c->ranks) {
+      HIP_TRY(hipSetDevice(q.dev));
+      for (Rank& s : c->ranks)
+        HIP_TRY(hipMemcpyAsync(q.gather + (size_t)s.rank * nb, s.totals16, sizeof(uint64_t) * nb, hipMemcpyDefault,
+                               q.stream));
+      LSB_TRY(chunk_plan(c, q, cs));
+    }
+  } else {
+    Rank& r = c->ranks[0];
+    {
+      Timer t(c, &r, LSB_K_EXCHANGE);
+      LSB_TRY(coll_allgather_u64(c, r, r.totals16, r.gather, nb));
+    }
+    LSB_TRY(chunk_plan(c, r, cs));
+  }
+  for (size_t i = 0; i < nr; ++i) {
+    Rank& r = c->ranks[i];
+    HIP_TRY(hipSetDevice(r.dev));
+    HIP_TRY(hipStreamSynchronize(r.stream));
+    plan_fetch(c, r);
+    LSB_TRY(chunk_geom(c, r, C, geo[i]));
+  }
+  if (loop)
+    for (size_t q = 0; q < nr; ++q)
+      for (size_t s = 0; s < nr; ++s)
+        for (int k = 0; k < C; ++k)
+          if (geo[s].send[q * C + k] != geo[q].recv[s * C + k])
+            return fail(LSB_ERR_STATE, "exchange_chunked", "send/recv count mismatch");
+  const bool self_in_r = c->self_coll && !loop;
+  // Where the next (gathered) pass finds each tile's records: peers' pieces
+  // in R, my own in Y, chunk k's at its own offset.
+  for (size_t i = 0; i < nr; ++i) {
+    Rank& r = c->ranks[i];
+    const int me = r.rank;
+    if (!r.gather_next) continue;
+    lsb::GatherSrc& g = r.gsrc;
+    g.R = r.R;
+    g.A = Y[i];
+    for (int k = 0; k < lsb::kMaxExchangeChunks; ++k)
+      g.self_adj[k] = k < C ? geo[i].lo[k] + geo[i].sdisp[(size_t)me * C + k] -
+                                  (r.recv_displs[me] + geo[i].rpre[(size_t)me * C + k])
+                            : 0;
+    g.chunk_shift = cs;
+    g.place = r.place;
+    g.gstart = r.gstart;
+    g.gadj = r.gstart + (size_t)P * nb;
+    g.desc = r.gdesc;
+    g.P = P;
+    g.nb = c->nb;
+    g.me = me;
+    g.self_in_a = !self_in_r;
+    HIP_TRY(hipSetDevice(r.dev));
+    Timer t(c, &r, LSB_K_EXCHANGE);
+    HIP_TRY(lsb::launch_gather_desc(g, r.here, r.gdesc, r.stream));
+  }
+  // RCCL calls of more than 1 GiB per peer are cut alike on every rank
+  // (coll_alltoallv_u64): the largest (peer, chunk) segment anywhere.
+  int64_t seg = 0;
+  if (!loop) {
+    Rank& r = c->ranks[0];
+    for (int q = 0; q < P; ++q)
+      if (q != r.rank || c->self_coll)
+        for (int k = 0; k < C; ++k)
+          seg = std::max(seg, std::max(geo[0].send[(size_t)q * C + k], geo[0].recv[(size_t)q * C + k]));
+    if (c->mode == Mode::kRccl && (size_t)c->per * 2 > max_call_u64()) {  // a chunk may hold the block
+      int64_t neg = -seg;
+      LSB_TRY(allreduce_min_i64(c, &neg));
+      seg = -neg;
+    } else {
+      seg = c->per;
+    }
+  }
+  // 3. chunk by chunk: the high-byte pass, then the wire
+  for (int k = 0; k < C; ++k) {
+    for (size_t i = 0; i < nr; ++i) {
+      Rank& r = c->ranks[i];
+      HIP_TRY(hipSetDevice(r.dev));
+      const int64_t lo = geo[i].lo[k], m = geo[i].lo[k + 1] - lo;
+      if (m > 0) {
+        // Chunk passes differ in tile count: each starts from zeroed look-back
+        // rows (epoch 1), and the next plain pass zeroes them all (os_dirty).
+        r.os_dirty = true;
+        HIP_TRY(hipMemsetAsync(r.os_status, 0, (size_t)lsb::onesweep_tiles(m) * lsb::kBuckets * sizeof(uint32_t),
+                               r.stream));
+        lsb::OnesweepExtra x;
+        x.halves = r.os_halves;
+        const int grid = std::max(lsb::kOnesweepSubs, (r.os_grid - c->xchunk_reserve) / 8 * 8);
+        hipError_t e;
+        {
+          Timer t(c, &r, LSB_K_SCATTER);
+          e = lsb::launch_onesweep(X[i] + lo, Y[i] + lo, m, hi_shift, -1,
+                                   r.ck_hist + (size_t)k * lsb::kOnesweepSubs * lsb::kBuckets, nullptr, r.os_status,
+                                   r.os_ctr, 1, r.os_ctr + lsb::kOnesweepSubs, grid, r.stream, x);
+        }
+        if (e != hipSuccess) {
+          (void)hipGetLastError();
+          return fail(LSB_ERR_HIP, "exchange_chunked: launch_onesweep", hipGetErrorString(e));
+        }
+        count_pass_elems(c, m);
+      }
+      HIP_TRY(hipEventRecord(r.ck_hi[k], r.stream));
+    }
+    if (loop) {
+      for (size_t q = 0; q < nr; ++q) {
+        Rank& rq = c->ranks[q];
+        HIP_TRY(hipSetDevice(rq.dev));
+        for (size_t s = 0; s < nr; ++s) HIP_TRY(hipStreamWaitEvent(rq.xstream, c->ranks[s].ck_hi[k], 0));
+        {
+          Timer t(c, &rq, LSB_K_WIRE, rq.xstream);
+          for (size_t s = 0; s < nr; ++s) {
+            if (s == q) continue;
+            const int64_t cnt = geo[q].recv[s * C + k];
+            if (cnt <= 0) continue;
+            const Elem* src = Y[s] + geo[s].lo[k] + geo[s].sdisp[q * C + k];
+            HIP_TRY(hipMemcpyAsync(rq.R + rq.recv_displs[s] + geo[q].rpre[s * C + k], src, (size_t)cnt * sizeof(Elem),
+                                   hipMemcpyDefault, rq.xstream));
+          }
+        }
+        HIP_TRY(hipEventRecord(rq.ck_wire[k], rq.xstream));
+      }
+    } else {
+      Rank& r = c->ranks[0];
+      const ChunkGeom& g = geo[0];
+      const int me = r.rank;
+      HIP_TRY(hipStreamWaitEvent(r.xstream, r.ck_hi[k], 0));
+      std::vector<size_t> sc(P), sd(P), rc(P), rdp(P);
+      for (int q = 0; q < P; ++q) {
+        const bool skip = q == me && !c->self_coll;
+        sc[q] = skip ? 0 : (size_t)g.send[(size_t)q * C + k] * 2;
+        rc[q] = skip ? 0 : (size_t)g.recv[(size_t)q * C + k] * 2;
+        sd[q] = (size_t)(g.lo[k] + g.sdisp[(size_t)q * C + k]) * 2;
+        rdp[q] = (size_t)(r.recv_displs[q] + g.rpre[(size_t)q * C + k]) * 2;
+      }
+      {
+        Timer t(c, &r, LSB_K_WIRE, r.xstream);
+        LSB_TRY(coll_alltoallv_u64(c, r, reinterpret_cast<const uint64_t*>(Y[0]), sc.data(), sd.data(),
+                                   reinterpret_cast<uint64_t*>(r.R), rc.data(), rdp.data(), (size_t)seg * 2,
+                                   r.xstream));
+      }
+      HIP_TRY(hipEventRecord(r.ck_wire[k], r.xstream));
+    }
+  }
+  // 4. placements, chunk k's once it has arrived (the last exchange's, which
+  //    write X, also once every chunk pass has read X)
+  for (size_t i = 0; i < nr; ++i) {
+    Rank& r = c->ranks[i];
+    const ChunkGeom& g = geo[i];
+    const int me = r.rank;
+    HIP_TRY(hipSetDevice(r.dev));
+    r.A = Y[i];  // the records, ordered by the digit chunk by chunk (my own segment's source)
+    r.B = X[i];  // the placement's destination
+    if (!r.gather_next) HIP_TRY(hipStreamWaitEvent(r.pstream, r.ck_hi[C - 1], 0));
+    for (int k = 0; k < C; ++k) {
+      HIP_TRY(hipStreamWaitEvent(r.pstream, r.ck_wire[k], 0));
+      for (int s = 0; s < P; ++s) {
+        const int64_t cnt = g.recv[(size_t)s * C + k];
+        const int64_t k0 = r.recv_displs[s] + g.rpre[(size_t)s * C + k];
+        if (s == me && !self_in_r)
+          LSB_TRY(place_range(c, r, shift, s, Y[i] + g.lo[k] + g.sdisp[(size_t)me * C + k], k0, cnt));
+        else
+          LSB_TRY(place_range(c, r, shift, s, r.R + k0, k0, cnt));
+      }
+    }
+    HIP_TRY(hipEventRecord(r.xdone, r.xstream));
+    HIP_TRY(hipStreamWaitEvent(r.stream, r.xdone, 0));
+    LSB_TRY(join_place_timed(c, r));
+    end_placement(r);
+  }
+  // Every rank's copies out of Y must be done before any rank's next pass
+  // rewrites it (loopback; RCCL ranks wait for their own wire stream above).
+  if (loop)
+    for (Rank& r : c->ranks) {
+      HIP_TRY(hipSetDevice(r.dev));
+      HIP_TRY(hipStreamSynchronize(r.stream));
+    }
+  return LSB_OK;
+}
+
 // ---- per-digit exchange with single-read local passes ----------------------
 // lsb_sort of the per-digit exchange forms (radix_bits 8 / 16, P > 1): the
 // reference's pass loop (mpi/mpi_lsbsort.cpp:580-585), each exchange digit's
@@ -582,19 +914,31 @@ int sort_exchange_onesweep(lsb_ctx* c) {
     }
     LSB_TRY(choose_halves(c, r, false));
   }
+  std::vector<const uint32_t*> lo_hist(c->ranks.size(), nullptr);
   for (size_t i = 0; i < steps.size(); ++i) {
     const Step& st = steps[i];
     const int after = i + 1 < steps.size() ? steps[i + 1].shift : -1;
-    // 16-bit digit: its high-byte pass counts the 65536 digits (a constant
-    // high byte leaves the count to digit_counts' read of A).
-    const bool c16 = c->bits == 16 && st.exch && st.shift == st.digit * 16 + lsb::kDigitBits;
-    begin_pass(c, st.shift);
-    for (Rank& r : c->ranks) {
-      lsb::OnesweepExtra x;
-      if (st.exch && c->bits == 8) x.totals = r.totals;
-      if (c16) x.count16 = r.totals16;
-      r.counts_ready = c16;
-      LSB_TRY(local_pass_os(c, r, st.shift, st.exch ? -1 : after, x));
+    // LSB_OPT_EXCHANGE_CHUNKS: the low byte's pass counts nothing for the next
+    // (exchange_chunked's read does), and the high byte's pass runs chunk by
+    // chunk inside exchange_chunked.
+    const bool chunked = chunked_applies(c, varying, st.digit);
+    if (chunked && st.exch) {
+      begin_pass(c, st.shift);
+    } else {
+      // 16-bit digit: its high-byte pass counts the 65536 digits (a constant
+      // high byte leaves the count to digit_counts' read of A).
+      const bool c16 = c->bits == 16 && st.exch && st.shift == st.digit * 16 + lsb::kDigitBits;
+      begin_pass(c, st.shift);
+      for (size_t k = 0; k < c->ranks.size(); ++k) {
+        Rank& r = c->ranks[k];
+        lsb::OnesweepExtra x;
+        if (st.exch && c->bits == 8) x.totals = r.totals;
+        if (c16) x.count16 = r.totals16;
+        r.counts_ready = c16;
+        LSB_TRY(local_pass_os(c, r, st.shift, st.exch || chunked ? -1 : after, x));
+        // the pass's input histogram (os_cur stays: next = -1): the chunk bounds
+        lo_hist[k] = r.os_hist + (size_t)r.os_cur * lsb::kOnesweepSubs * lsb::kBuckets;
+      }
     }
     ++c->last_local_passes;
     if (!st.exch) continue;
@@ -611,7 +955,7 @@ int sort_exchange_onesweep(lsb_ctx* c) {
       }
     }
     ++c->last_exchanges;
-    const int rc = exchange_digit(c, st.digit);
+    const int rc = chunked ? exchange_chunked(c, st.digit, lo_hist) : exchange_digit(c, st.digit);
     for (Rank& r : c->ranks) {
       if (rc == LSB_OK && r.place_next >= 0) {
         r.os_cur ^= 1;

@@ -152,7 +152,10 @@ struct SegPass {
 // (digit, source) order) lies in piece e = b * P + s (bucket b's records from
 // source s), the last e with gstart[e] <= p; its record is
 //   R[p - place[s * nb + b]]                          (a peer's piece)
-//   A[p - place[s * nb + b] + self_adj]               (s == me, self_in_a)
+//   A[p - place[s * nb + b] + self_adj[chunk of b]]   (s == me, self_in_a)
+// (chunk of b: (b & 255) >> chunk_shift; the per-digit exchange in chunks,
+// launch_count16_chunks, keeps the rank's own records in C chunk ranges of A;
+// unchunked, chunk_shift = 8: one chunk.)
 // TileDesc caches that per onesweep tile: up to 4 pieces (first position
 // relative to the tile, pointer adjustment, bit j of sel: piece j is in A);
 // n = kDescOverflow sends the tile's records to the search over [e0, e1].
@@ -163,10 +166,12 @@ struct alignas(16) TileDesc {
   int32_t start[kDescPieces];
   int64_t adj[kDescPieces];
 };
+constexpr int kMaxExchangeChunks = 8;
 struct GatherSrc {
   const Elem* R = nullptr;
   const Elem* A = nullptr;
-  int64_t self_adj = 0;
+  int64_t self_adj[kMaxExchangeChunks] = {};
+  int chunk_shift = 8;
   const int64_t* place = nullptr;  // P * nb place_off (launch_plan)
   const int64_t* gstart = nullptr;  // P * nb piece starts (launch_plan)
   const int64_t* gadj = nullptr;    // P * nb scratch: 2 * pointer adjustment + (1: in A)
@@ -176,6 +181,19 @@ struct GatherSrc {
 // gadj, then desc[t] for every onesweep tile of m records (after launch_plan
 // with gstart).
 hipError_t launch_gather_desc(const GatherSrc& g, int64_t m, TileDesc* desc, hipStream_t s);
+// The per-digit exchange in chunks (LSB_OPT_EXCHANGE_CHUNKS, 16-bit digits;
+// DESIGN.md §6): after the low-byte pass of digit d, B (m records) is sorted
+// by the low byte l; chunk k = the records with l in [k << cshift,
+// (k + 1) << cshift), a contiguous range of B (C = 256 >> cshift chunks).  One
+// read of B gives count16[(h << 8) | l] (zeroed here: the digit's 65536
+// counts, for the exchange plan) and chunk_hist[(k * 8 + x) * 256 + h]
+// (zeroed here: the high byte's sub-array histogram over chunk k's own tiles,
+// the sub_hist of chunk k's high-byte pass), so the plan and the sends can
+// precede the high-byte pass, which then runs chunk by chunk while the
+// previous chunk is on the wire.  lo_hist: the low byte's sub-array
+// histogram (its totals give the chunk bounds).  shift16 = 16 * d.
+hipError_t launch_count16_chunks(const Elem* B, int64_t m, int shift16, const uint32_t* lo_hist, int cshift,
+                                 int grid, uint64_t* count16, uint32_t* chunk_hist, hipStream_t s);
 // Regional first pass (P == 1 LSD sorts of at least kRegionMin records,
 // LSB_OPT_REGION_FIRST): the sort's first pass needs no
 // histogram read.  Its records of digit b from sub-array x go to region
@@ -315,10 +333,15 @@ hipError_t launch_system_acquire(hipStream_t s);
 // recv counts), counts[0..P) = send counts, counts[P..2P) = recv counts.
 // work: P * nb int64, total: nb int64 scratch.  gstart (optional, P * nb):
 // gstart[b * P + s] = first position of piece (b, s) in my block, clamped to
-// [0, here] (nondecreasing in b * P + s).
+// [0, here] (nondecreasing in b * P + s).  cshift < 8 (the chunked exchange,
+// nb = 65536, C = 256 >> cshift chunks of the low byte): a source's pieces
+// lie in R in chunk order (chunk of l, h, l) instead of digit order, which
+// place_off follows, and chunk_counts[q * C + k] = my records of chunk k for
+// owner q, chunk_counts[P * C + s * C + k] = source s's records of chunk k
+// for me.
 hipError_t launch_plan(const uint64_t* hist, int P, int nb, int me, int64_t n, int64_t* work,
                        int64_t* total, int64_t* place, int64_t* counts, hipStream_t s,
-                       int64_t* gstart = nullptr);
+                       int64_t* gstart = nullptr, int cshift = 8, int64_t* chunk_counts = nullptr);
 
 // ---- whole-key exchange (radix_bits = 64; lsb_merge.hip) ----
 // Splitter search: for Q targets T_t, state[2t .. 2t+1] = key interval

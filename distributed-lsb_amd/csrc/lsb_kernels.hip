@@ -636,7 +636,8 @@ __device__ __forceinline__ int gather_piece(const GatherSrc& g, int e0, int e1, 
 __device__ __forceinline__ int64_t gather_adj(const GatherSrc& g, int e) {
   const int src = e % g.P, b = e / g.P;
   const bool in_a = src == g.me && g.self_in_a;
-  return 2 * ((in_a ? g.self_adj : 0) - g.place[(int64_t)src * g.nb + b]) + (in_a ? 1 : 0);
+  return 2 * ((in_a ? g.self_adj[(b & (kBuckets - 1)) >> g.chunk_shift] : 0) - g.place[(int64_t)src * g.nb + b]) +
+         (in_a ? 1 : 0);
 }
 __device__ __forceinline__ const Elem* gather_search(const GatherSrc& g, int e0, int e1, int64_t p) {
   const int64_t v = g.gadj[gather_piece(g, e0, e1, p)];
@@ -734,6 +735,113 @@ __global__ __launch_bounds__(BLOCK) void k_subhist(const Elem* __restrict__ A, i
       atomicOr(&span[1], (unsigned long long)no);
     }
   }
+}
+
+// k_count16c (launch_count16_chunks, the chunked per-digit exchange): B is
+// sorted by the low byte l, so a tile holds one l and one (chunk, sub-array)
+// except at the ~256 + 8 C tiles across a boundary.  The tile's high-byte
+// counts (per-wave LDS rows) are added to a running row per target -- count16
+// of l, chunk_hist of (k, x) -- flushed to global memory when the target
+// changes; a tile across a boundary adds record by record to global memory.
+// Workgroup c walks tiles [c * tpw, (c + 1) * tpw).
+template <int BLOCK, int IPT>
+__global__ __launch_bounds__(BLOCK) void k_count16c(const Elem* __restrict__ B, int64_t m, int shift16,
+                                                    const uint32_t* __restrict__ lo_hist, int cshift,
+                                                    int64_t tiles_per_wg, unsigned long long* __restrict__ count16,
+                                                    uint32_t* __restrict__ chunk_hist) {
+  constexpr int W = BLOCK / 64;
+  constexpr int T = BLOCK * IPT;
+  static_assert(BLOCK == kBuckets, "thread t owns high byte t");
+  __shared__ uint32_t th[W][kBuckets];
+  __shared__ int64_t tot[kBuckets];
+  __shared__ int64_t cstart[kMaxExchangeChunks + 1];
+  const int t = threadIdx.x, w = t >> 6;
+  const int C = kBuckets >> cshift;
+  {
+    int64_t v = 0;
+#pragma unroll
+    for (int x = 0; x < kSub; ++x) v += lo_hist[x * kBuckets + t];
+    tot[t] = v;
+    for (int ww = 0; ww < W; ++ww) th[ww][t] = 0;
+  }
+  __syncthreads();
+  if (t <= C) {
+    int64_t a = 0;
+    for (int l = 0; l < (t << cshift) && l < kBuckets; ++l) a += tot[l];
+    cstart[t] = a;
+  }
+  __syncthreads();
+  const uint64_t* __restrict__ keys = reinterpret_cast<const uint64_t*>(B);
+  const int64_t TT = (m + T - 1) / T;
+  const int64_t t0 = (int64_t)blockIdx.x * tiles_per_wg;
+  const int64_t t1 = t0 + tiles_per_wg < TT ? t0 + tiles_per_wg : TT;
+  // (chunk, sub-array) of position p whose low byte is l
+  auto target = [&](int64_t p, uint32_t l) -> uint32_t {
+    const uint32_t k = l >> cshift;
+    const int64_t len = cstart[k + 1] - cstart[k];
+    const int64_t TTk = (len + T - 1) / T;
+    return k * kSub + (uint32_t)sub_of_tile((p - cstart[k]) / T, TTk);
+  };
+  uint32_t cur_l = 0xFFFFFFFFu, cur_s = 0xFFFFFFFFu;  // the running rows' targets
+  uint32_t acc_l = 0, acc_s = 0;                      // thread t: bin t of each row
+  auto flush_l = [&]() {
+    if (cur_l != 0xFFFFFFFFu && acc_l) atomicAdd(&count16[((uint32_t)t << 8) | cur_l], (unsigned long long)acc_l);
+    acc_l = 0;
+  };
+  auto flush_s = [&]() {
+    if (cur_s != 0xFFFFFFFFu && acc_s) atomicAdd(&chunk_hist[cur_s * kBuckets + t], acc_s);
+    acc_s = 0;
+  };
+  for (int64_t tile = t0; tile < t1; ++tile) {
+    const int64_t tb = tile * T;
+    const int64_t end = tb + T < m ? tb + T : m;
+    const uint32_t lf = (uint32_t)(keys[2 * tb] >> shift16) & 0xFFu;
+    const uint32_t ll = (uint32_t)(keys[2 * (end - 1)] >> shift16) & 0xFFu;
+    const uint32_t sf = target(tb, lf), sl = target(end - 1, ll);
+    const bool uniform = lf == ll && sf == sl;  // the same for the whole workgroup
+    uint64_t k[IPT];
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+      const int64_t idx = tb + (int64_t)i * BLOCK + t;
+      k[i] = idx < end ? __builtin_nontemporal_load(keys + 2 * idx) : 0ull;  // streaming
+    }
+    if (uniform) {
+#pragma unroll
+      for (int i = 0; i < IPT; ++i) {
+        const int64_t idx = tb + (int64_t)i * BLOCK + t;
+        if (idx < end) atomicAdd(&th[w][(uint32_t)(k[i] >> (shift16 + 8)) & 0xFFu], 1u);
+      }
+      __syncthreads();
+      uint32_t v = 0;
+#pragma unroll
+      for (int ww = 0; ww < W; ++ww) {
+        v += th[ww][t];
+        th[ww][t] = 0;
+      }
+      if (lf != cur_l) {
+        flush_l();
+        cur_l = lf;
+      }
+      if (sf != cur_s) {
+        flush_s();
+        cur_s = sf;
+      }
+      acc_l += v;
+      acc_s += v;
+      __syncthreads();
+    } else {
+#pragma unroll
+      for (int i = 0; i < IPT; ++i) {
+        const int64_t idx = tb + (int64_t)i * BLOCK + t;
+        if (idx >= end) continue;
+        const uint32_t l = (uint32_t)(k[i] >> shift16) & 0xFFu, h = (uint32_t)(k[i] >> (shift16 + 8)) & 0xFFu;
+        atomicAdd(&count16[(h << 8) | l], 1ull);
+        atomicAdd(&chunk_hist[target(idx, l) * kBuckets + h], 1u);
+      }
+    }
+  }
+  flush_l();
+  flush_s();
 }
 
 // The regional first pass's sample (launch_sample): workgroup g reads tile
@@ -1757,10 +1865,13 @@ __global__ __launch_bounds__(256) void k_plan_cols(const uint64_t* __restrict__ 
 
 constexpr int kPlanScanBlock = 1024;
 
-// Exclusive scan of v[0..len) in place by one workgroup, returns the sum.
+// Exclusive scan of v[idx(0..len)) in place by one workgroup, in the order
+// idx gives (the identity, or the chunked exchange's order), returns the sum.
 // Segments of 4 * kPlanScanBlock entries; thread t owns 4 consecutive
-// entries of a segment, so every load and store is coalesced.
-__device__ int64_t block_scan_inplace(int64_t* v, int len, int64_t* tmp) {
+// entries of a segment, so every load and store is coalesced (for the
+// chunked order: runs of 2^cshift consecutive entries).
+template <typename Idx>
+__device__ int64_t block_scan_inplace(int64_t* v, int len, int64_t* tmp, Idx idx) {
   constexpr int V = 4;
   int64_t carry = 0;
   for (int seg = 0; seg < len; seg += V * kPlanScanBlock) {
@@ -1769,14 +1880,14 @@ __device__ int64_t block_scan_inplace(int64_t* v, int len, int64_t* tmp) {
     int64_t s = 0;
 #pragma unroll
     for (int j = 0; j < V; ++j) {
-      x[j] = i0 + j < len ? v[i0 + j] : 0;
+      x[j] = i0 + j < len ? v[idx(i0 + j)] : 0;
       s += x[j];
     }
     int64_t tot;
     int64_t pre = carry + block_exclusive_scan<kPlanScanBlock>(s, tmp, &tot);
 #pragma unroll
     for (int j = 0; j < V; ++j) {
-      if (i0 + j < len) v[i0 + j] = pre;
+      if (i0 + j < len) v[idx(i0 + j)] = pre;
       pre += x[j];
     }
     carry += tot;
@@ -1786,21 +1897,25 @@ __device__ int64_t block_scan_inplace(int64_t* v, int len, int64_t* tmp) {
 
 __global__ __launch_bounds__(kPlanScanBlock) void k_plan_base(int64_t* __restrict__ total, int nb) {
   __shared__ int64_t tmp[kPlanScanBlock / 64];
-  block_scan_inplace(total, nb, tmp);  // total -> base
+  block_scan_inplace(total, nb, tmp, [](int i) { return i; });  // total -> base
 }
 
+// cshift < 8 (the chunked exchange): also the send counts per (owner q,
+// chunk k of b) into chunk_send[q * C + k].
 __global__ __launch_bounds__(256) void k_plan_pieces(const uint64_t* __restrict__ hist, int P, int nb,
                                                      int me, int64_t per, int64_t lo, int64_t hi,
                                                      const int64_t* __restrict__ base,
                                                      int64_t* __restrict__ work,
                                                      int64_t* __restrict__ place,
                                                      unsigned long long* __restrict__ send_counts,
-                                                     int64_t* __restrict__ gstart) {
+                                                     int64_t* __restrict__ gstart, int cshift,
+                                                     unsigned long long* __restrict__ chunk_send) {
   // Send counts are summed per workgroup in LDS first: every bucket of a
   // rank adds to the same few owners, and 65536 same-address global
   // atomics took 0.8 ms.
-  __shared__ unsigned long long sc[64];
-  if (threadIdx.x < 64) sc[threadIdx.x] = 0;
+  __shared__ unsigned long long sc[64 * kMaxExchangeChunks];
+  const int C = kBuckets >> cshift;  // 1 unchunked
+  for (int i = threadIdx.x; i < 64 * kMaxExchangeChunks; i += 256) sc[i] = 0;
   __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i < (int64_t)P * nb) {
@@ -1818,25 +1933,52 @@ __global__ __launch_bounds__(256) void k_plan_pieces(const uint64_t* __restrict_
       gstart[(int64_t)b * P + s] = l;
     }
     if (s == me && h > 0) {
+      const int k = (b & (kBuckets - 1)) >> cshift;
       int64_t g = g0;
       while (g < g1) {  // split my run over its owners
         const int64_t q = g / per;
         const int64_t qend = g1 < (q + 1) * per ? g1 : (q + 1) * per;
-        atomicAdd(&sc[q], (unsigned long long)(qend - g));
+        atomicAdd(&sc[q * C + k], (unsigned long long)(qend - g));
         g = qend;
       }
     }
   }
   __syncthreads();
-  if ((int)threadIdx.x < P && sc[threadIdx.x])
-    atomicAdd(&send_counts[threadIdx.x], sc[threadIdx.x]);
+  for (int i = threadIdx.x; i < P * C; i += 256) {
+    if (!sc[i]) continue;
+    atomicAdd(&send_counts[i / C], sc[i]);
+    if (chunk_send) atomicAdd(&chunk_send[i], sc[i]);
+  }
 }
 
+// cshift < 8 (the chunked exchange, nb = 65536): source s's pieces scanned
+// in chunk order -- (chunk of the low byte, high byte, low byte), the order
+// its records arrive in R -- and chunk_recv[s * C + k] = the records of chunk
+// k it sends me.
 __global__ __launch_bounds__(kPlanScanBlock) void k_plan_rows(int64_t* __restrict__ work, int nb,
-                                                              int64_t* __restrict__ recv_counts) {
+                                                              int64_t* __restrict__ recv_counts, int cshift,
+                                                              int64_t* __restrict__ chunk_recv) {
   __shared__ int64_t tmp[kPlanScanBlock / 64];
   const int s = blockIdx.x;
-  const int64_t tot = block_scan_inplace(work + (int64_t)s * nb, nb, tmp);
+  int64_t* row = work + (int64_t)s * nb;
+  int64_t tot;
+  if (cshift >= 8) {
+    tot = block_scan_inplace(row, nb, tmp, [](int i) { return i; });
+  } else {
+    const int lw = 1 << cshift;
+    tot = block_scan_inplace(row, nb, tmp, [=](int i) {
+      const int k = i >> (8 + cshift), h = (i >> cshift) & (kBuckets - 1), l = (k << cshift) | (i & (lw - 1));
+      return (h << 8) | l;
+    });
+    __syncthreads();
+    const int C = kBuckets >> cshift;
+    if ((int)threadIdx.x < C) {
+      const int k = threadIdx.x;
+      const int64_t a = row[k << cshift];  // the first digit of chunk k in that order: (h 0, l = k << cshift)
+      const int64_t e = k + 1 < C ? row[(k + 1) << cshift] : tot;
+      chunk_recv[(int64_t)s * C + k] = e - a;
+    }
+  }
   if (threadIdx.x == 0) recv_counts[s] = tot;
 }
 
@@ -2053,6 +2195,22 @@ hipError_t launch_subhist(const Elem* A, int64_t m, int shift, int grid, uint32_
   return hipGetLastError();
 }
 
+hipError_t launch_count16_chunks(const Elem* B, int64_t m, int shift16, const uint32_t* lo_hist, int cshift,
+                                 int grid, uint64_t* count16, uint32_t* chunk_hist, hipStream_t s) {
+  if (shift16 < 0 || shift16 > 48 || cshift < 5 || cshift > 7 || !lo_hist) return hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(count16, 0, sizeof(uint64_t) * 65536, s);
+  if (e == hipSuccess)
+    e = hipMemsetAsync(chunk_hist, 0, sizeof(uint32_t) * (kBuckets >> cshift) * kSub * kBuckets, s);
+  if (e != hipSuccess || m <= 0) return e;
+  const int64_t TT = (m + kTile - 1) / kTile;
+  if (grid < 1) grid = 1;
+  const int64_t tpw = (TT + grid - 1) / grid;
+  hipLaunchKernelGGL((k_count16c<kScatterBlock, kScatterIpt>), dim3((unsigned)((TT + tpw - 1) / tpw)),
+                     dim3(kScatterBlock), 0, s, B, m, shift16, lo_hist, cshift, tpw,
+                     reinterpret_cast<unsigned long long*>(count16), chunk_hist);
+  return hipGetLastError();
+}
+
 hipError_t launch_sample(const Elem* A, int64_t m, int shift, uint32_t* hist, uint64_t* span, hipStream_t s) {
   if (shift < 0 || shift > 56) return hipErrorInvalidValue;
   hipError_t e = hipMemsetAsync(hist, 0, sizeof(uint32_t) * kBuckets, s);
@@ -2246,8 +2404,14 @@ hipError_t launch_system_acquire(hipStream_t s) {
 
 hipError_t launch_plan(const uint64_t* hist, int P, int nb, int me, int64_t n, int64_t* work,
                        int64_t* total, int64_t* place, int64_t* counts, hipStream_t s,
-                       int64_t* gstart) {
+                       int64_t* gstart, int cshift, int64_t* chunk_counts) {
   if (P < 1 || me < 0 || me >= P || nb < 1 || n < 0) return hipErrorInvalidValue;
+  if (cshift < 8 && (nb != 65536 || cshift < 5 || !chunk_counts || P > 64)) return hipErrorInvalidValue;
+  const int C = cshift < 8 ? kBuckets >> cshift : 1;
+  if (cshift < 8) {
+    hipError_t e = hipMemsetAsync(chunk_counts, 0, sizeof(int64_t) * 2 * P * C, s);
+    if (e != hipSuccess) return e;
+  }
   const int64_t per = (n + P - 1) / P;
   const int64_t lo = (int64_t)me * per;
   int64_t here = n - lo;
@@ -2261,8 +2425,10 @@ hipError_t launch_plan(const uint64_t* hist, int P, int nb, int me, int64_t n, i
   hipLaunchKernelGGL(k_plan_base, dim3(1), dim3(kPlanScanBlock), 0, s, total, nb);
   hipLaunchKernelGGL(k_plan_pieces, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, s, hist, P,
                      nb, me, per, lo, hi, total, work, place,
-                     reinterpret_cast<unsigned long long*>(counts), gstart);
-  hipLaunchKernelGGL(k_plan_rows, dim3(P), dim3(kPlanScanBlock), 0, s, work, nb, counts + P);
+                     reinterpret_cast<unsigned long long*>(counts), gstart, cshift < 8 ? cshift : 8,
+                     cshift < 8 ? reinterpret_cast<unsigned long long*>(chunk_counts) : nullptr);
+  hipLaunchKernelGGL(k_plan_rows, dim3(P), dim3(kPlanScanBlock), 0, s, work, nb, counts + P, cshift < 8 ? cshift : 8,
+                     cshift < 8 ? chunk_counts + (size_t)P * C : nullptr);
   hipLaunchKernelGGL(k_plan_finish, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, s, P, nb,
                      lo, work, counts + P, place);
   return hipGetLastError();

@@ -123,6 +123,19 @@ struct Rank {
   int64_t* gstart = nullptr;            // [nb][P] piece starts in the placed order
   lsb::TileDesc* gdesc = nullptr;       // [tiles]
   lsb::GatherSrc gsrc;
+  // The per-digit exchange in chunks (LSB_OPT_EXCHANGE_CHUNKS, lsb_exchange.cpp
+  // exchange_chunked), allocated on first use: the wire stream, chunk k's
+  // events (its high-byte pass done on `stream`, its records received on
+  // xstream), the count kernel's per-chunk histograms and the plan's
+  // per-chunk counts (device, pinned mirror), the low byte's histogram mirror.
+  hipStream_t xstream = nullptr;
+  hipEvent_t ck_hi[lsb::kMaxExchangeChunks] = {};
+  hipEvent_t ck_wire[lsb::kMaxExchangeChunks] = {};
+  hipEvent_t xdone = nullptr;
+  uint32_t* ck_hist = nullptr;          // [C][8][256]
+  int64_t* ck_counts = nullptr;         // [2][P][C]: send per (owner, chunk), recv per (source, chunk)
+  int64_t* ck_counts_h = nullptr;
+  uint32_t* lo_hist_h = nullptr;        // [8][256]
   // Whole-key exchange (radix_bits = 64), allocated on first use.
   uint64_t* split_state = nullptr;      // [Q][2] key interval per target
   int64_t* split_targets = nullptr;     // [Q] global positions q * per
@@ -156,6 +169,8 @@ struct lsb_ctx {
   bool force_exchange = false;
   bool skip_constant = true;  // lsb_sort skips digits on which all keys agree
   int slices = 0;             // exchange slices (placement overlaps the next slice); 0 = default
+  int xchunks = 0;            // LSB_OPT_EXCHANGE_CHUNKS: 16-bit exchange digits in C chunks (0: off)
+  int xchunk_reserve = 0;     // LSB_XCHUNK_RESERVE: workgroups the chunk passes leave to the wire
   bool p2p = false;           // RCCL exchange as grouped ncclSend/ncclRecv, not ncclAllToAllv
   bool peer = false;          // exchange by direct stores into the owners' buffers
   bool peer_ready = false;    // peer tables set up
@@ -328,7 +343,7 @@ constexpr size_t kMaxCallU64 = (size_t)1 << 27;
 size_t max_call_u64();
 int coll_alltoallv_u64(lsb_ctx* c, Rank& r, const uint64_t* send, const size_t* sc,
                        const size_t* sd, uint64_t* recv, const size_t* rc, const size_t* rd,
-                       size_t bound);
+                       size_t bound, hipStream_t stream = nullptr);
 int gather_boundaries(lsb_ctx* c, std::vector<uint64_t>& bnd);
 int allreduce_min_i64(lsb_ctx* c, int64_t* v);
 int gather_span(lsb_ctx* c, uint64_t* kor, uint64_t* knor);
@@ -407,6 +422,12 @@ int ensure_recv(lsb_ctx* c, Rank& r);
 int join_place(Rank& r);
 int join_place_timed(lsb_ctx* c, Rank& r);
 int exchange_digit(lsb_ctx* c, int digit);
+// The per-digit exchange in chunks: digit `digit` (16 bits) whose low-byte
+// pass has run (A sorted by the low byte; lo_hist its input's sub-array
+// histogram on each rank), high-byte passes chunk by chunk, each chunk's
+// records on the wire while the next chunk's pass runs.
+bool chunked_applies(const lsb_ctx* c, uint64_t varying, int digit);
+int exchange_chunked(lsb_ctx* c, int digit, const std::vector<const uint32_t*>& lo_hist);
 bool exchange_onesweep_applies(const lsb_ctx* c);
 int sort_exchange_onesweep(lsb_ctx* c);
 

@@ -55,6 +55,7 @@ OPT_HYBRID = 9
 OPT_EXCHANGE_GATHER = 10
 OPT_FAIL_ONESWEEP = 11
 OPT_REGION_FIRST = 12
+OPT_EXCHANGE_CHUNKS = 13
 FIRST_COUNT, FIRST_REGIONAL, FIRST_REGIONAL_REDONE = 0, 1, 2
 MAX_PASSES = 16
 

@@ -147,6 +147,15 @@ typedef struct lsb_ctx lsb_ctx_t;
                                       overflows all the same makes the sort start over from
                                       its input.  0: every sort starts with the histogram
                                       read.  Same output. */
+#define LSB_OPT_EXCHANGE_CHUNKS 13 /* radix_bits = 16 exchanges (P > 1 or forced; RCCL or loopback):
+                                      C = 2, 4 or 8 sends each digit's records in C chunks of
+                                      its low byte while the high-byte pass runs chunk by chunk
+                                      (chunk k's records on the wire during chunk k + 1's pass;
+                                      mpi/mpi_lsbsort.cpp:481-577 runs localShuffle, then the
+                                      whole exchange).  One read after the low-byte pass counts
+                                      the digit first.  0 (default; the
+                                      environment's LSB_EXCHANGE_CHUNKS sets a context's start
+                                      value) sends after the whole pass.  Same output. */
 
 /* ---- geometry: DistributedArray::create (mpi/mpi_lsbsort.cpp:144-149) ---- */
 int64_t lsb_per_rank(int64_t n_total, int num_ranks);            /* ceil(n/P) */
