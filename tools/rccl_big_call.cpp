@@ -19,6 +19,7 @@
 #include <sys/wait.h>
 #include <unistd.h>
 
+#include <array>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -142,16 +143,14 @@ int main(int argc, char** argv) {
   else forms = {argv[2]};
   std::vector<size_t> mib;
   for (int i = 3; i < argc; ++i) mib.push_back((size_t)atoll(argv[i]));
-  int version = 0;
-  (void)ncclGetVersion(&version);
-  printf("{\"rccl_version\": %d, \"world\": %d}\n", version, world);
-  fflush(stdout);
-  // The id before any HIP call (ncclGetUniqueId opens a bootstrap socket only);
-  // the ranks are forked children, each initialising HIP itself.
-  ncclUniqueId id;
-  if (ncclGetUniqueId(&id) != ncclSuccess) return 1;
+  // No RCCL or HIP call in the parent (ncclGetUniqueId initialises the
+  // runtime, and a forked child of an initialised parent cannot use the
+  // GPU): rank 0 makes the id and hands it to the others through pipes.
   int fds[2];
   if (pipe(fds) != 0) return 1;
+  std::vector<std::array<int, 2>> idp(world);
+  for (auto& p : idp)
+    if (pipe(p.data()) != 0) return 1;
   std::vector<pid_t> kids;
   for (int r = 0; r < world; ++r) {
     const pid_t p = fork();
@@ -162,6 +161,21 @@ int main(int argc, char** argv) {
       setenv("NCCL_HOSTID", host, 1);
       setenv("NCCL_SOCKET_IFNAME", "lo", 0);
       setenv("NCCL_IB_DISABLE", "1", 0);
+      ncclUniqueId id;
+      if (r == 0) {
+        if (ncclGetUniqueId(&id) != ncclSuccess) _exit(5);
+        for (int q = 1; q < world; ++q)
+          if (write(idp[q][1], &id, sizeof id) != (ssize_t)sizeof id) _exit(5);
+      } else if (read(idp[r][0], &id, sizeof id) != (ssize_t)sizeof id) {
+        _exit(5);
+      }
+      if (r == 0) {
+        int version = 0;
+        (void)ncclGetVersion(&version);
+        char line[128];
+        const int len = snprintf(line, sizeof line, "{\"rccl_version\": %d, \"world\": %d}\n", version, world);
+        if (write(fds[1], line, (size_t)len) != len) _exit(4);
+      }
       const int rank = r;
       const int rc = run_rank(rank, world, id, forms, mib, fds[1]);
       _exit(rc);
