@@ -592,7 +592,16 @@ int lsb_get_exchange_bytes(lsb_ctx_t* c, int64_t* calls, int64_t* bytes, int64_t
 #ifndef LSB_BUILD_HOST
 #define LSB_BUILD_HOST "unknown"
 #endif
-const char* lsb_build_info(void) { return "sha256=" LSB_SOURCE_DIGEST " host=" LSB_BUILD_HOST; }
+const char* lsb_build_info(void) {
+  // The RCCL the process loaded (ncclGetVersion touches no device): its large
+  // calls are cut at 1 GiB per peer (coll_alltoallv_u64).
+  static const std::string info = [] {
+    int v = 0;
+    (void)ncclGetVersion(&v);
+    return std::string("sha256=" LSB_SOURCE_DIGEST " host=" LSB_BUILD_HOST " rccl=") + std::to_string(v);
+  }();
+  return info.c_str();
+}
 
 // Host planner: see include/lsb.h.  For rank `me`, the global destination of
 // its j-th bucket-b record is gstart[b][me] + j with

@@ -262,20 +262,19 @@ int alloc_candidates(const lsb_ctx* c, size_t per, int K, size_t need, std::vect
 }  // namespace
 
 // Times one k_onesweep pass x -> y over the rank's here records on the byte
-// at `shift`, with the rank's own look-back rows and histograms
-// (onesweep_ensure); the histogram read before it is not timed.
-// hist: kOnesweepSubs * 256 u32 of scratch (r.os_hist at creation; a buffer
-// of its own once a sort may hold a histogram in r.os_hist).
-double time_pass(Rank& r, Prober& pr, const Elem* x, Elem* y, int shift, uint32_t* hist) {
+// at `shift` (its sub-array histogram in hist_in), counting the byte at
+// next_shift over y into hist_out for the next pass of a chain, with the
+// rank's own look-back rows (onesweep_ensure).
+double time_pass(Rank& r, Prober& pr, const Elem* x, Elem* y, int shift, int next_shift, const uint32_t* hist_in,
+                 uint32_t* hist_out) {
   if (pr.err != hipSuccess) return 0.0;
-  pr.err = lsb::launch_subhist(x, r.here, shift, r.os_grid, hist, nullptr, r.stream);
   uint32_t epoch = r.os_epoch + 1;
   if (epoch >= (1u << 30)) epoch = 2;  // as onesweep_launch: keep the parity alternation
-  if (pr.err == hipSuccess) pr.err = hipEventRecord(pr.e0, r.stream);
+  pr.err = hipEventRecord(pr.e0, r.stream);
   lsb::OnesweepExtra probe;
   probe.probe = true;  // k_onesweep_probe: the same pass under its own name (profiles)
   if (pr.err == hipSuccess)
-    pr.err = lsb::launch_onesweep(x, y, r.here, shift, -1, hist, nullptr, r.os_status, r.os_ctr, epoch,
+    pr.err = lsb::launch_onesweep(x, y, r.here, shift, next_shift, hist_in, hist_out, r.os_status, r.os_ctr, epoch,
                                   r.os_ctr + lsb::kOnesweepSubs, r.os_grid, r.stream, probe);
   if (pr.err == hipSuccess) r.os_epoch = epoch;
   if (pr.err == hipSuccess) pr.err = hipEventRecord(pr.e1, r.stream);
@@ -285,12 +284,42 @@ double time_pass(Rank& r, Prober& pr, const Elem* x, Elem* y, int shift, uint32_
   return t;
 }
 
-// A and B.  The probe is the pass itself: each candidate gets uniform PCG
-// keys, and one k_onesweep pass is timed between every ordered pair (on a
-// byte the source is not ordered by).  A copy with the same write pattern
-// (tools/kbench/allocbw.hip) ranked the buffers by their streaming write speed, but
-// that did not predict the pass, whose tile loads sit on its look-back chain
-// (profiles/r04/placement_*.log, pick.log).
+namespace {
+
+// A chain of timed passes: each moves the latest records from the buffer
+// holding them into `dst`, on the next byte, with the histogram the pass
+// before counted (one k_subhist read at the start only).
+struct Chain {
+  Rank& r;
+  Prober& pr;
+  uint32_t* h[2];
+  int cur = 0, shift = 0;
+  Elem* holder;
+  Chain(Rank& r_, Prober& pr_, uint32_t* hist2, Elem* first) : r(r_), pr(pr_), h{hist2, hist2 + lsb::kOnesweepSubs * lsb::kBuckets}, holder(first) {
+    if (pr.err == hipSuccess) pr.err = lsb::launch_subhist(first, r.here, 0, r.os_grid, h[0], nullptr, r.stream);
+  }
+  double pass(Elem* dst) {
+    const int next = (shift + lsb::kDigitBits) & 63;
+    const double t = time_pass(r, pr, holder, dst, shift, next, h[cur], h[cur ^ 1]);
+    cur ^= 1;
+    shift = next;
+    holder = dst;
+    return t;
+  }
+};
+
+struct Samples {
+  double sum = 0.0;
+  int n = 0;
+  double mean() const { return n ? sum / n : 1e300; }
+  void add(double t) {
+    sum += t;
+    ++n;
+  }
+};
+
+}  // namespace
+
 // After a probe: a probe pass that gave up on its look-back leaves the sort's
 // give-up word set and its status rows of an older parity.  Start them over
 // (as onesweep_check does) and fail the creation rather than hand the next
@@ -326,16 +355,19 @@ int64_t record_capacity(int64_t per, int P) {
   return cap > 0 ? std::max(per, lsb::region_stride(cap) * lsb::kRegions) : per;
 }
 
-// The probe times each candidate once, as a destination: a buffer of pieces
-// is slow or fast as the destination of the LSD write pattern as a whole,
-// whatever the source (tools/kbench/pairbw2.hip), so the
-// round-5 matrix of K(K - 1) ordered pairs measured the same thing K - 1
-// times.  X (PCG keys) and Y come first, each timed as the other's
-// destination; every further candidate Z is timed as the destination of the
-// buffer holding the latest records, and whichever of the two kept buffers is
-// the slower destination is freed at once (or Z, if it is slower than both).
-// K timed passes (and one warm-up), and at most three buffers live: the
-// probe's transient memory is one buffer (round 5: K - 2 at once).
+// The probe times each candidate as a destination: a buffer of pieces is
+// slow or fast as the destination of the LSD write pattern as a whole,
+// whatever the source (tools/kbench/pairbw2.hip), so round 5's
+// matrix of a timed pass between every ordered pair of K candidates measured
+// each destination K - 1 times and held all K buffers at once.  Here the
+// passes form one chain (each pass's input histogram counted by the pass
+// before it, so one k_subhist read in all): X (PCG keys) and Y first, each
+// twice a destination; then every further candidate Z twice a destination
+// (holder -> Z -> kept -> Z -> kept), and whichever of the two kept buffers is
+// the slower destination on average is freed at once (or Z, if it is slower
+// than both).  4K - 3 passes (13 at K = 4) and one histogram read (round 5:
+// 13 passes and 13 reads); at most three buffers live: the probe's transient
+// memory is one buffer (round 5: K - 2 at once).
 int alloc_records(lsb_ctx* c, Rank& r) {
   const size_t per = (size_t)record_capacity(c->per, c->P);
   r.cap = (int64_t)per;
@@ -364,14 +396,15 @@ int alloc_records(lsb_ctx* c, Rank& r) {
   const bool pick_worst = pick && strcmp(pick, "worst") == 0;
   auto better = [&](double a, double b) { return pick_worst ? a > b : a < b; };
   Prober pr(r.stream, r.here);
-  pr.err = lsb::launch_pcg_fill(keep[0], r.here, 0x5eed, 0, lsb::KeyGen(), r.stream);
-  (void)time_pass(r, pr, keep[0], keep[1], 0, r.os_hist);  // warm-up
-  double ms[2];
-  ms[1] = time_pass(r, pr, keep[0], keep[1], 0, r.os_hist);  // Y as destination
-  ms[0] = time_pass(r, pr, keep[1], keep[0], 8, r.os_hist);  // X as destination (Y is ordered by byte 0)
-  const double first_pair = 0.5 * (ms[0] + ms[1]);
-  double worst = std::max(ms[0], ms[1]);
-  int src = 0, shift = 16;  // keep[src] holds the latest records, ordered by byte shift - 8
+  if (pr.err == hipSuccess) pr.err = lsb::launch_pcg_fill(keep[0], r.here, 0x5eed, 0, lsb::KeyGen(), r.stream);
+  std::vector<Samples> sm(2);  // per candidate, in allocation order
+  int ki[2] = {0, 1};          // the kept buffers' candidate numbers
+  Chain ch(r, pr, r.os_hist, keep[0]);
+  (void)ch.pass(keep[1]);  // warm-up
+  for (int i = 0; i < 2; ++i) {
+    sm[0].add(ch.pass(keep[0]));
+    sm[1].add(ch.pass(keep[1]));
+  }
   int tried = 2;
   for (; tried < K && pr.err == hipSuccess; ++tried) {
     if (rec_alloc(c, &z, per) != LSB_OK) {  // fewer candidates than hoped
@@ -379,15 +412,18 @@ int alloc_records(lsb_ctx* c, Rank& r) {
       z = nullptr;
       break;
     }
-    const double t = time_pass(r, pr, keep[src], z, shift, r.os_hist);
-    shift = (shift + 8) & 63;
-    worst = std::max(worst, t);
-    const int slow = better(ms[0], ms[1]) ? 1 : 0;
-    if (better(t, ms[slow])) {  // z replaces the slower kept buffer and holds the latest records
+    sm.emplace_back();
+    Samples& sz = sm.back();
+    sz.add(ch.pass(z));
+    sm[ki[0]].add(ch.pass(keep[0]));
+    sz.add(ch.pass(z));
+    sm[ki[1]].add(ch.pass(keep[1]));  // the records are in keep[1] again
+    const int slow = better(sm[ki[0]].mean(), sm[ki[1]].mean()) ? 1 : 0;
+    if (better(sz.mean(), sm[ki[slow]].mean())) {  // z replaces the slower kept buffer
+      if (ch.holder == keep[slow]) (void)ch.pass(z);  // move the records out of it first
       rec_free(keep[slow]);
       keep[slow] = z;
-      ms[slow] = t;
-      src = slow;
+      ki[slow] = tried;
     } else {
       rec_free(z);
     }
@@ -396,10 +432,12 @@ int alloc_records(lsb_ctx* c, Rank& r) {
   if (pr.err != hipSuccess) return give_up(fail(LSB_ERR_HIP, "alloc_records: placement probe", hipGetErrorString(pr.err)));
   rc = probe_check(r);
   if (rc != LSB_OK) return give_up(rc);
+  double worst = 0.0;
+  for (const Samples& x : sm) worst = std::max(worst, x.mean());
   r.placement_k = tried;
-  r.placement_ms[0] = 0.5 * (ms[0] + ms[1]);
-  r.placement_ms[1] = first_pair;  // the first two buffers allocated
-  r.placement_ms[2] = worst;       // the slowest destination timed
+  r.placement_ms[0] = 0.5 * (sm[ki[0]].mean() + sm[ki[1]].mean());
+  r.placement_ms[1] = 0.5 * (sm[0].mean() + sm[1].mean());  // the first two buffers allocated
+  r.placement_ms[2] = worst;                                  // the slowest destination (mean)
   r.A = keep[0];
   r.B = keep[1];
   return LSB_OK;
@@ -407,11 +445,12 @@ int alloc_records(lsb_ctx* c, Rank& r) {
 
 // The third record buffer R (receive buffer of the exchanges, the hybrid's
 // third pass buffer), placed like A and B: among up to 3 candidates, the
-// fastest destination of a timed pass out of B (scratch whenever R is first
-// needed: before a hybrid sort, at an exchange before its placement), each
-// loser freed at once (two buffers live at most).  A may hold records by then
-// and is not touched; the probe counts into a histogram of its own, since a
-// sort may hold one in r.os_hist.
+// fastest destination (twice each, in a chain of passes between B and the
+// candidate; B is scratch whenever R is first needed: before a hybrid sort,
+// at an exchange before its placement), each loser freed at once (two
+// buffers live at most).  A may hold records by then and is not touched; the
+// chain counts into histograms of its own, since a sort may hold one in
+// r.os_hist.
 int alloc_third(lsb_ctx* c, Rank& r) {
   // As many records as A and B: the hybrid permutes the three buffers, and
   // the regional first pass writes into whichever one is B by then.
@@ -420,9 +459,10 @@ int alloc_third(lsb_ctx* c, Rank& r) {
   if (K <= 2) K = 1;
   if (K == 1 || !r.os_status) return rec_alloc(c, &r.R, per);
   uint32_t* hist = nullptr;
-  LSB_TRY(dev_alloc(&hist, (size_t)lsb::kOnesweepSubs * lsb::kBuckets));
+  LSB_TRY(dev_alloc(&hist, (size_t)2 * lsb::kOnesweepSubs * lsb::kBuckets));
   Prober pr(r.stream, r.here);
   pr.err = lsb::launch_pcg_fill(r.B, r.here, 0x5eed + 16, 0, lsb::KeyGen(), r.stream);
+  Chain ch(r, pr, hist, r.B);
   Elem* best = nullptr;
   double best_ms = 1e300;
   int rc = LSB_OK;
@@ -432,11 +472,15 @@ int alloc_third(lsb_ctx* c, Rank& r) {
       (void)hipGetLastError();
       break;
     }
-    const double t = time_pass(r, pr, r.B, z, 0, hist);
-    if (t < best_ms) {
+    Samples sz;
+    sz.add(ch.pass(z));
+    (void)ch.pass(r.B);
+    sz.add(ch.pass(z));
+    (void)ch.pass(r.B);  // the records are in B again
+    if (sz.mean() < best_ms) {
       rec_free(best);
       best = z;
-      best_ms = t;
+      best_ms = sz.mean();
     } else {
       rec_free(z);
     }

@@ -248,11 +248,17 @@ int coll_allgather_u64(lsb_ctx* c, Rank& r, const uint64_t* send, uint64_t* recv
 // MPI_Alltoallv semantics in uint64 units (counts and displacements).
 // `bound`: a count no rank sends to any peer in this call exceeds (the same on
 // every rank: every rank must issue the same RCCL calls).  RCCL moves a
-// per-peer range of 2 GiB or more wrongly (the world-of-one exchange at 2^28
-// records per rank, 2 GiB in its first slice, verified false; 512 MiB per
-// call verified: profiles/r05/x16dbg_probe.log), so an RCCL call whose bound
-// exceeds kMaxCallU64 goes as ceil(bound / kMaxCallU64) calls, call i
-// carrying part i of every peer's range on both sides.  (The reference's
+// per-peer range of 2 GiB or more wrongly in a world of one (the x16 exchange
+// at 2^28 records per rank, 2 GiB in its first slice, verified false:
+// profiles/r05/x16dbg_probe.log; and RCCL alone, tools/rccl_big_call.cpp, RCCL
+// 2.27.7: of a 2 GiB or 4 GiB range the second half comes back wrong, with
+// ncclAllToAllv and with grouped ncclSend / ncclRecv; 512 MiB and 1 GiB
+// right: profiles/r06/rccl_big/world1.jsonl).  Two ranks over RCCL's socket
+// transport moved 2 and 4 GiB per peer, self ranges included, correctly
+// (world2.jsonl); xGMI is untested here, so the cut stays at N > 1 too (at
+// N = 8 with 2^30 uniform records per GPU no call is cut).  An RCCL call whose
+// bound exceeds max_call_u64() goes as ceil(bound / max_call_u64()) calls,
+// call i carrying part i of every peer's range on both sides.  (The reference's
 // MPI_Alltoallv takes int counts and cannot pass 2^31 records at all,
 // mpi/mpi_lsbsort.cpp:292-313.)
 size_t max_call_u64() {

@@ -1547,7 +1547,7 @@ __global__ __launch_bounds__(BLOCK, (HALVES == 1 ? 2 : 3) * BLOCK / 256) void k_
 }
 
 // The placement probe's pass (lsb_context.cpp alloc_records): the same code
-// as k_onesweep's last-pass instance under its own name, so that profiles
+// as k_onesweep's next-counting instance under its own name, so that profiles
 // and the bench's PMC passes keep the probe launches at context creation
 // apart from the sort's.
 __global__ __launch_bounds__(kOsBlock, 2 * kOsBlock / 256) void k_onesweep_probe(
@@ -1556,9 +1556,9 @@ __global__ __launch_bounds__(kOsBlock, 2 * kOsBlock / 256) void k_onesweep_probe
     uint32_t* __restrict__ status, uint32_t* __restrict__ tile_ctr, uint32_t epoch,
     uint32_t* __restrict__ err, uint64_t* __restrict__ totals,
     unsigned long long* __restrict__ count16, SegPass seg, GatherSrc gs) {
-  onesweep_body<kOsBlock, kOsIpt, false, false, 1, false, false, 0>(in, out, m, shift, next_shift, sub_hist,
-                                                                    next_hist, status, tile_ctr, epoch, err,
-                                                                    totals, count16, seg, gs, RegionPass());
+  onesweep_body<kOsBlock, kOsIpt, true, false, 1, false, false, 0>(in, out, m, shift, next_shift, sub_hist,
+                                                                   next_hist, status, tile_ctr, epoch, err,
+                                                                   totals, count16, seg, gs, RegionPass());
 }
 
 // ------------------------------------------------------------------- place
@@ -2298,10 +2298,13 @@ hipError_t launch_onesweep(const Elem* in, Elem* out, int64_t m, int shift, int 
                          gsrc, rp);
     }
   } else if (extra.probe) {
-    // The placement probe: a last pass, whole stage, under its own name.
-    if (next_shift >= 0 || c16 || extra.halves != 1 || extra.seg || gat) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_onesweep_probe, gd, bd, 0, s, in, out, m, shift, 0, sub_hist, nullptr, st, tile_ctr,
-                       epoch, err, nullptr, nullptr, SegPass(), gsrc);
+    // The placement probe: a pass counting the next digit (the sort's usual
+    // instance), whole stage, under its own name.
+    if (next_shift < 0 || !next_hist || c16 || extra.halves != 1 || extra.seg || gat) return hipErrorInvalidValue;
+    e = hipMemsetAsync(next_hist, 0, sizeof(uint32_t) * kSub * kBuckets, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_onesweep_probe, gd, bd, 0, s, in, out, m, shift, next_shift, sub_hist, next_hist, st,
+                       tile_ctr, epoch, err, nullptr, nullptr, SegPass(), gsrc);
   } else if (extra.seg) {
     // The hybrid's last pass: no next digit, no 16-bit counts, whole stage.
     if (next_shift >= 0 || c16 || extra.halves != 1 || !extra.seg->base ||

@@ -232,7 +232,8 @@ def device_memory(dev: int = 0) -> tuple:
 
 def build_info() -> dict:
     """{"sha256": digest of the sources the loaded library was built from,
-    "host": build host} (lsb_build_info)."""
+    "host": build host, "rccl": ncclGetVersion of the loaded RCCL}
+    (lsb_build_info)."""
     info = _lib().lsb_build_info().decode()
     return dict(kv.split("=", 1) for kv in info.split())
 

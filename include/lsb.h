@@ -383,7 +383,8 @@ int  lsb_device_memory(int dev, int64_t* free_bytes, int64_t* total_bytes);
 
 /* ---- build --------------------------------------------------------------- */
 /* "sha256=<digest of the sources the library was built from> host=<build
- * host>" (static string).  tests/ compare the digest with the tree. */
+ * host> rccl=<ncclGetVersion of the RCCL loaded>" (static string).  tests/
+ * compare the digest with the tree. */
 const char* lsb_build_info(void);
 
 /* ---- host planner (pure host code; used by the runtime when P > 1) ------- */
