@@ -103,14 +103,18 @@ def parse():
     ap.add_argument("--exchange", choices=("alltoallv", "p2p", "peer"), default="alltoallv",
                     help="N > 1 element exchange: RCCL AllToAllv in slices (default), grouped "
                          "ncclSend/ncclRecv, or direct peer stores into the owners' buffers")
+    ap.add_argument("--exchange-chunks", type=int, choices=(0, 2, 4, 8), default=0,
+                    help="16-bit exchange digits sent in C chunks while the high-byte pass runs chunk by "
+                         "chunk (LSB_OPT_EXCHANGE_CHUNKS; 0: after the whole pass).  N > 1 reports C = 8 "
+                         "as the chunked_* extra")
     ap.add_argument("--zipf-s", type=float, default=1.1)
     ap.add_argument("--passes", choices=("onesweep", "reduce-scan", "hybrid"), default="onesweep",
                     help="local pass form: single-read (look-back), count + scan + scatter, or the "
                          "hybrid (single-read passes on the top bytes, then one segmented local sort; "
                          "LSB_OPT_HYBRID, P = 1 and the whole-key form's local sorts)")
     ap.add_argument("--no-extras", action="store_true",
-                    help="skip the extra forms timed after the headline (hybrid and x16 at N = 1, whole key "
-                         "and peer at N > 1)")
+                    help="skip the extra forms timed after the headline (hybrid and x16 at N = 1, whole key, "
+                         "peer and chunked at N > 1)")
     ap.add_argument("--force-exchange", action="store_true",
                     help="N = 1: run the exchange path anyway, over a world-of-one RCCL communicator that "
                          "carries every record through ncclAllToAllv (LSB_OPT_FORCE_EXCHANGE + "
@@ -437,6 +441,8 @@ def make_world(a, d, N, n_total, radix):
         w.set_option(lsbsort.OPT_EXCHANGE_PEER, 1)
     w.set_option(lsbsort.OPT_ONESWEEP, 0 if a.passes == "reduce-scan" else 1)
     w.set_option(lsbsort.OPT_HYBRID, 1 if a.passes == "hybrid" else 0)
+    if a.exchange_chunks:
+        w.set_option(lsbsort.OPT_EXCHANGE_CHUNKS, a.exchange_chunks)
     return w, device
 
 
@@ -596,6 +602,10 @@ def extras_at(a, N):
         out.append(("whole_key", whole_key_argv(a)))
     if radix != 64 and a.exchange != "peer" and not a.no_peer and a.transport != "gloo":
         out.append(("peer", peer_argv(a)))
+    # the 16-bit exchange in chunks (LSB_OPT_EXCHANGE_CHUNKS = 8): each chunk's
+    # records on the wire while the next chunk's high-byte pass runs
+    if radix == 16 and a.exchange == "alltoallv" and not a.exchange_chunks and a.transport != "gloo":
+        out.append(("chunked", extra_argv(a, ["--exchange-chunks", "8"])))
     return out
 
 
@@ -702,7 +712,8 @@ def dry_run(a):
         sys.exit(3)
     top = d.max(float(d.rank))
     form = ("x16" if a.force_exchange else "whole_key" if radix == 64 and d.world > 1 else
-            "peer" if a.exchange == "peer" else "hybrid" if a.passes == "hybrid" else "headline")
+            "peer" if a.exchange == "peer" else "hybrid" if a.passes == "hybrid" else
+            "chunked" if a.exchange_chunks else "headline")
     out = {"metric": METRIC, "value": float(d.world * radix), "ms_per_step": 1.0,
            "verified": form != a.dry_unverified,
            "n_gpus": d.world, "max_rank": top, "radix_bits": radix, "exchange": a.exchange,

@@ -222,3 +222,17 @@ def test_eight_rank_memory_fits_the_device(candidates):
     assert 48 * gib <= m["bytes"] < 49 * gib  # A, B, R of 16 GiB each + 1/64 look-back rows
     assert m["probe_bytes"] == 16 * gib  # one candidate beside A and B at a time, whatever K
     assert m["device_bytes"] == 288 * 10**9 and m["fits"] and m["peak_frac"] < 0.9
+
+
+def test_chunked_extra_at_n2():
+    """N > 1 with 16-bit digits: the chunked exchange (LSB_OPT_EXCHANGE_CHUNKS =
+    8) is timed as the chunked_* extra beside the headline, verified like the
+    others; a wrong chunked output fails the run."""
+    r = _bench(["--gpus", "2", "--dry-rank", "--no-cpu-baseline", "--steps", "2", "--no-whole-key", "--no-peer"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = _line(r.stdout)
+    assert out["chunked_melem_s"] == 2 * 16 and out["chunked_verified"] is True
+    r = _bench(["--gpus", "2", "--dry-rank", "--no-cpu-baseline", "--steps", "2", "--no-whole-key", "--no-peer",
+                "--dry-unverified", "chunked"])
+    assert r.returncode == 1
+    assert _line(r.stdout)["chunked_verified"] is False
