@@ -308,16 +308,6 @@ struct Chain {
   }
 };
 
-struct Samples {
-  double sum = 0.0;
-  int n = 0;
-  double mean() const { return n ? sum / n : 1e300; }
-  void add(double t) {
-    sum += t;
-    ++n;
-  }
-};
-
 }  // namespace
 
 // After a probe: a probe pass that gave up on its look-back leaves the sort's
@@ -355,19 +345,22 @@ int64_t record_capacity(int64_t per, int P) {
   return cap > 0 ? std::max(per, lsb::region_stride(cap) * lsb::kRegions) : per;
 }
 
-// The probe times each candidate as a destination: a buffer of pieces is
-// slow or fast as the destination of the LSD write pattern as a whole,
+// The probe times each candidate once, as a destination: a buffer of pieces
+// is slow or fast as the destination of the LSD write pattern as a whole,
 // whatever the source (tools/kbench/pairbw2.hip), so round 5's
 // matrix of a timed pass between every ordered pair of K candidates measured
 // each destination K - 1 times and held all K buffers at once.  Here the
 // passes form one chain (each pass's input histogram counted by the pass
-// before it, so one k_subhist read in all): X (PCG keys) and Y first, each
-// twice a destination; then every further candidate Z twice a destination
-// (holder -> Z -> kept -> Z -> kept), and whichever of the two kept buffers is
-// the slower destination on average is freed at once (or Z, if it is slower
-// than both).  4K - 3 passes (13 at K = 4) and one histogram read (round 5:
-// 13 passes and 13 reads); at most three buffers live: the probe's transient
-// memory is one buffer (round 5: K - 2 at once).
+// before it: one k_subhist read in all): X (PCG keys) and Y first, each once
+// a destination; then every further candidate Z once (the holder of the
+// records -> Z), and whichever of the two kept buffers is the slower
+// destination is freed at once -- or Z, after one more pass moves the
+// records back into a kept buffer.  At most 2K - 1 passes (7 at K = 4; round
+// 5: 13 passes and 13 histogram reads) and three buffers live: the probe's
+// transient memory is one buffer (round 5: K - 2 at once).  Interleaved with
+// round 5's form in fresh processes, 53.65-53.92 ms per sort against
+// 53.66-53.90 (profiles/r06/probe/); a form timing every candidate twice
+// gave the same (53.66-53.86) for 0.05 s more creation time.
 int alloc_records(lsb_ctx* c, Rank& r) {
   const size_t per = (size_t)record_capacity(c->per, c->P);
   r.cap = (int64_t)per;
@@ -397,14 +390,13 @@ int alloc_records(lsb_ctx* c, Rank& r) {
   auto better = [&](double a, double b) { return pick_worst ? a > b : a < b; };
   Prober pr(r.stream, r.here);
   if (pr.err == hipSuccess) pr.err = lsb::launch_pcg_fill(keep[0], r.here, 0x5eed, 0, lsb::KeyGen(), r.stream);
-  std::vector<Samples> sm(2);  // per candidate, in allocation order
-  int ki[2] = {0, 1};          // the kept buffers' candidate numbers
   Chain ch(r, pr, r.os_hist, keep[0]);
   (void)ch.pass(keep[1]);  // warm-up
-  for (int i = 0; i < 2; ++i) {
-    sm[0].add(ch.pass(keep[0]));
-    sm[1].add(ch.pass(keep[1]));
-  }
+  double ms[2];
+  ms[0] = ch.pass(keep[0]);
+  ms[1] = ch.pass(keep[1]);  // the records are in keep[1]
+  const double first_pair = 0.5 * (ms[0] + ms[1]);
+  double worst = std::max(ms[0], ms[1]);
   int tried = 2;
   for (; tried < K && pr.err == hipSuccess; ++tried) {
     if (rec_alloc(c, &z, per) != LSB_OK) {  // fewer candidates than hoped
@@ -412,19 +404,15 @@ int alloc_records(lsb_ctx* c, Rank& r) {
       z = nullptr;
       break;
     }
-    sm.emplace_back();
-    Samples& sz = sm.back();
-    sz.add(ch.pass(z));
-    sm[ki[0]].add(ch.pass(keep[0]));
-    sz.add(ch.pass(z));
-    sm[ki[1]].add(ch.pass(keep[1]));  // the records are in keep[1] again
-    const int slow = better(sm[ki[0]].mean(), sm[ki[1]].mean()) ? 1 : 0;
-    if (better(sz.mean(), sm[ki[slow]].mean())) {  // z replaces the slower kept buffer
-      if (ch.holder == keep[slow]) (void)ch.pass(z);  // move the records out of it first
+    const double t = ch.pass(z);  // the records are in z
+    worst = std::max(worst, t);
+    const int slow = better(ms[0], ms[1]) ? 1 : 0;
+    if (better(t, ms[slow])) {  // z replaces the slower kept buffer
       rec_free(keep[slow]);
       keep[slow] = z;
-      ki[slow] = tried;
+      ms[slow] = t;
     } else {
+      (void)ch.pass(keep[0]);  // the records back into a kept buffer
       rec_free(z);
     }
     z = nullptr;
@@ -432,12 +420,10 @@ int alloc_records(lsb_ctx* c, Rank& r) {
   if (pr.err != hipSuccess) return give_up(fail(LSB_ERR_HIP, "alloc_records: placement probe", hipGetErrorString(pr.err)));
   rc = probe_check(r);
   if (rc != LSB_OK) return give_up(rc);
-  double worst = 0.0;
-  for (const Samples& x : sm) worst = std::max(worst, x.mean());
   r.placement_k = tried;
-  r.placement_ms[0] = 0.5 * (sm[ki[0]].mean() + sm[ki[1]].mean());
-  r.placement_ms[1] = 0.5 * (sm[0].mean() + sm[1].mean());  // the first two buffers allocated
-  r.placement_ms[2] = worst;                                  // the slowest destination (mean)
+  r.placement_ms[0] = 0.5 * (ms[0] + ms[1]);
+  r.placement_ms[1] = first_pair;  // the first two buffers allocated
+  r.placement_ms[2] = worst;       // the slowest destination timed
   r.A = keep[0];
   r.B = keep[1];
   return LSB_OK;
@@ -445,7 +431,7 @@ int alloc_records(lsb_ctx* c, Rank& r) {
 
 // The third record buffer R (receive buffer of the exchanges, the hybrid's
 // third pass buffer), placed like A and B: among up to 3 candidates, the
-// fastest destination (twice each, in a chain of passes between B and the
+// fastest destination (once each, in a chain of passes between B and the
 // candidate; B is scratch whenever R is first needed: before a hybrid sort,
 // at an exchange before its placement), each loser freed at once (two
 // buffers live at most).  A may hold records by then and is not touched; the
@@ -472,15 +458,12 @@ int alloc_third(lsb_ctx* c, Rank& r) {
       (void)hipGetLastError();
       break;
     }
-    Samples sz;
-    sz.add(ch.pass(z));
-    (void)ch.pass(r.B);
-    sz.add(ch.pass(z));
+    const double t = ch.pass(z);
     (void)ch.pass(r.B);  // the records are in B again
-    if (sz.mean() < best_ms) {
+    if (t < best_ms) {
       rec_free(best);
       best = z;
-      best_ms = sz.mean();
+      best_ms = t;
     } else {
       rec_free(z);
     }

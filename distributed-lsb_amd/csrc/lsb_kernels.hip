@@ -921,6 +921,13 @@ __device__ unsigned long long g_os_prof[10];
 // workgroup); uniform keys 4.7 % slower (two more barriers per tile, half-
 // length write phases): profiles/ab/r02_ab12_*.
 //
+// Neighbours each way a SEG walk loads together before walking on (LSB_SEG_WIN;
+// 0: the plain one-read-at-a-time walk).
+#ifndef LSB_SEG_WIN
+#define LSB_SEG_WIN 2
+#endif
+constexpr int kSegWin = LSB_SEG_WIN;
+
 // SEG (the hybrid's last pass, SegPass in lsb_kernels.h): the write-out also
 // orders each segment (records equal on seg.pmask; inside the tile they are
 // adjacent in the stage, in one bucket run) by the whole key: a record's slot
@@ -1458,11 +1465,32 @@ __device__ __forceinline__ void onesweep_body(
           const bool sp = j > 0 && (pv & seg.pmask) == pk;
           const bool sn = j + 1 < nvalid && (nx & seg.pmask) == pk;
           if (sp || sn) {
-            // Walk the segment in LDS (bounded: kSegMax each way).
+            // Walk the segment in LDS (bounded: kSegMax each way).  The first
+            // kSegWin neighbours each way are loaded together (independent
+            // LDS reads; segments hold ~2 records at the runtime's bytes), and
+            // the walk goes on one read at a time only past them.  Out of
+            // range, a neighbour reads as ~v.key, outside the segment.
             uint32_t less = 0, eqb = 0;
-            int k = j - 1;
             const int klo = j - kSegMax > 0 ? j - kSegMax : 0;
-            while (k >= klo) {
+            const int khi = j + 1 + kSegMax < nvalid ? j + 1 + kSegMax : nvalid;
+            uint64_t wb[kSegWin > 0 ? kSegWin : 1], wf[kSegWin > 0 ? kSegWin : 1];
+#pragma unroll
+            for (int q = 0; q < kSegWin; ++q) {
+              wb[q] = j - 1 - q >= klo ? stage[j - 1 - q].key : ~v.key;
+              wf[q] = j + 1 + q < khi ? stage[j + 1 + q].key : ~v.key;
+            }
+            int k = j - 1;
+            bool on = true;
+#pragma unroll
+            for (int q = 0; q < kSegWin; ++q) {
+              on = on && (wb[q] & seg.pmask) == pk;
+              if (on) {
+                less += wb[q] < v.key ? 1u : 0u;
+                eqb += wb[q] == v.key ? 1u : 0u;
+                --k;
+              }
+            }
+            while (on && k >= klo) {
               const uint64_t kk = stage[k].key;
               if ((kk & seg.pmask) != pk) break;
               less += kk < v.key ? 1u : 0u;
@@ -1472,9 +1500,17 @@ __device__ __forceinline__ void onesweep_body(
             const int sfirst = k + 1;  // the segment's first stage slot
             // kSegMax records walked without leaving the segment: too long
             bool too_long = k < klo && klo > 0;
-            const int khi = j + 1 + kSegMax < nvalid ? j + 1 + kSegMax : nvalid;
             k = j + 1;
-            while (k < khi) {
+            on = true;
+#pragma unroll
+            for (int q = 0; q < kSegWin; ++q) {
+              on = on && (wf[q] & seg.pmask) == pk;
+              if (on) {
+                less += wf[q] < v.key ? 1u : 0u;
+                ++k;
+              }
+            }
+            while (on && k < khi) {
               const uint64_t kk = stage[k].key;
               if ((kk & seg.pmask) != pk) break;
               less += kk < v.key ? 1u : 0u;
