@@ -927,6 +927,11 @@ __device__ unsigned long long g_os_prof[10];
 #define LSB_SEG_WIN 2
 #endif
 constexpr int kSegWin = LSB_SEG_WIN;
+// The SEG instance's whole tiles through the batched write-out (records, then
+// their delta entries, read LSB_SEG_BATCH at a time first; 0: one by one).
+#ifndef LSB_SEG_BATCH
+#define LSB_SEG_BATCH 4
+#endif
 
 // SEG (the hybrid's last pass, SegPass in lsb_kernels.h): the write-out also
 // orders each segment (records equal on seg.pmask; inside the tile they are
@@ -1419,6 +1424,83 @@ __device__ __forceinline__ void onesweep_body(
     };
     // The write-out is instantiated twice (the launch-uniform `skewed` picks
     // one outside it): a per-record branch on it cost uniform keys 2.4 %.
+    // SEG: record v's slot in its tile stage (pos = j unless a stage
+    // neighbour shares its segment): its segment's first stage slot +
+    // #(segment keys < v) + #(equal keys staged before v).  Lanes of a wave
+    // hold consecutive j, so the neighbours are the next lanes (DPP).
+    auto seg_pos = [&](const Elem& v, int j, int jend) -> int {
+      int pos = j;
+      // Stage neighbours j - 1 and j + 1 are the neighbouring lanes'
+      // records (the wave's j are consecutive; lanes 0 and 63 read LDS).
+      const uint32_t kl = (uint32_t)v.key, kh = (uint32_t)(v.key >> 32);
+      uint64_t pv = ((uint64_t)(uint32_t)__builtin_amdgcn_update_dpp(0, (int)kh, 0x138, 0xf, 0xf, false) << 32) |
+                    (uint32_t)__builtin_amdgcn_update_dpp(0, (int)kl, 0x138, 0xf, 0xf, false);
+      uint64_t nx = ((uint64_t)(uint32_t)__builtin_amdgcn_update_dpp(0, (int)kh, 0x130, 0xf, 0xf, false) << 32) |
+                    (uint32_t)__builtin_amdgcn_update_dpp(0, (int)kl, 0x130, 0xf, 0xf, false);
+      if (lane == 0 && j > 0) pv = stage[j - 1].key;
+      if ((lane == 63 || j + 1 == jend) && j + 1 < nvalid) nx = stage[j + 1].key;
+      const uint64_t pk = v.key & seg.pmask;
+      const bool sp = j > 0 && (pv & seg.pmask) == pk;
+      const bool sn = j + 1 < nvalid && (nx & seg.pmask) == pk;
+      if (sp || sn) {
+        // Walk the segment in LDS (bounded: kSegMax each way).  The first
+        // kSegWin neighbours each way are loaded together (independent
+        // LDS reads; segments hold ~2 records at the runtime's bytes), and
+        // the walk goes on one read at a time only past them.  Out of
+        // range, a neighbour reads as ~v.key, outside the segment.
+        uint32_t less = 0, eqb = 0;
+        const int klo = j - kSegMax > 0 ? j - kSegMax : 0;
+        const int khi = j + 1 + kSegMax < nvalid ? j + 1 + kSegMax : nvalid;
+        uint64_t wb[kSegWin > 0 ? kSegWin : 1], wf[kSegWin > 0 ? kSegWin : 1];
+#pragma unroll
+        for (int q = 0; q < kSegWin; ++q) {
+          wb[q] = j - 1 - q >= klo ? stage[j - 1 - q].key : ~v.key;
+          wf[q] = j + 1 + q < khi ? stage[j + 1 + q].key : ~v.key;
+        }
+        int k = j - 1;
+        bool on = true;
+#pragma unroll
+        for (int q = 0; q < kSegWin; ++q) {
+          on = on && (wb[q] & seg.pmask) == pk;
+          if (on) {
+            less += wb[q] < v.key ? 1u : 0u;
+            eqb += wb[q] == v.key ? 1u : 0u;
+            --k;
+          }
+        }
+        while (on && k >= klo) {
+          const uint64_t kk = stage[k].key;
+          if ((kk & seg.pmask) != pk) break;
+          less += kk < v.key ? 1u : 0u;
+          eqb += kk == v.key ? 1u : 0u;
+          --k;
+        }
+        const int sfirst = k + 1;  // the segment's first stage slot
+        // kSegMax records walked without leaving the segment: too long
+        bool too_long = k < klo && klo > 0;
+        k = j + 1;
+        on = true;
+#pragma unroll
+        for (int q = 0; q < kSegWin; ++q) {
+          on = on && (wf[q] & seg.pmask) == pk;
+          if (on) {
+            less += wf[q] < v.key ? 1u : 0u;
+            ++k;
+          }
+        }
+        while (on && k < khi) {
+          const uint64_t kk = stage[k].key;
+          if ((kk & seg.pmask) != pk) break;
+          less += kk < v.key ? 1u : 0u;
+          ++k;
+        }
+        too_long |= k == khi && khi < nvalid;
+        // 2: this tile's slots may collide (not a permutation, SegPass).
+        if (too_long) atomicOr(seg.err, 2u);
+        pos = sfirst + (int)(less + eqb);
+      }
+      return pos;
+    };
     auto write_out = [&](auto skew_tag, int h) {
       const int jend = HALVES == 1 || (h + 1) * HT >= nvalid ? nvalid : (h + 1) * HT;
       // A whole tile: every thread's T / BLOCK records read from the stage
@@ -1426,14 +1508,17 @@ __device__ __forceinline__ void onesweep_body(
       // overlap instead of serialising twice per record (-0.6...-0.9 % per
       // sort, profiles/r04/ab_wo/).  Only the LSD passes' whole-stage
       // instances: the exchange's and the split stage's would spill.
-      if (!SEG && HALVES == 1 && !C16 && !GATHER && jend == HT) {
-        constexpr int G = HT / BLOCK;
-        {
+      if ((!SEG || LSB_SEG_BATCH) && HALVES == 1 && !C16 && !GATHER && jend == HT) {
+        // G records per batch (the SEG instance: LSB_SEG_BATCH at a time, so
+        // its walk registers fit beside them).
+        constexpr int G = SEG && LSB_SEG_BATCH > 0 && LSB_SEG_BATCH < HT / BLOCK ? LSB_SEG_BATCH : HT / BLOCK;
+#pragma unroll
+        for (int k0 = 0; k0 < HT / BLOCK; k0 += G) {
           Elem v[G];
           int64_t dl[G];
           uint32_t ct[G];
 #pragma unroll
-          for (int k = 0; k < G; ++k) v[k] = stage[k * BLOCK + t];
+          for (int k = 0; k < G; ++k) v[k] = stage[(k0 + k) * BLOCK + t];
 #pragma unroll
           for (int k = 0; k < G; ++k) {
             const uint32_t d = (uint32_t)(v[k].key >> shift) & (kBuckets - 1);
@@ -1442,8 +1527,8 @@ __device__ __forceinline__ void onesweep_body(
           }
 #pragma unroll
           for (int k = 0; k < G; ++k) {
-            const int j = k * BLOCK + t;
-            emit(skew_tag, v[k], j, dl[k] + j, ct[k]);
+            const int j = (k0 + k) * BLOCK + t;
+            emit(skew_tag, v[k], j, dl[k] + (SEG ? seg_pos(v[k], j, jend) : j), ct[k]);
           }
         }
         return;
@@ -1451,77 +1536,7 @@ __device__ __forceinline__ void onesweep_body(
       for (int j = h * HT + t; j < jend; j += BLOCK) {
         const Elem v = stage[j - h * HT];
         int pos = j;
-        if (SEG) {
-          // Stage neighbours j - 1 and j + 1 are the neighbouring lanes'
-          // records (the wave's j are consecutive; lanes 0 and 63 read LDS).
-          const uint32_t kl = (uint32_t)v.key, kh = (uint32_t)(v.key >> 32);
-          uint64_t pv = ((uint64_t)(uint32_t)__builtin_amdgcn_update_dpp(0, (int)kh, 0x138, 0xf, 0xf, false) << 32) |
-                        (uint32_t)__builtin_amdgcn_update_dpp(0, (int)kl, 0x138, 0xf, 0xf, false);
-          uint64_t nx = ((uint64_t)(uint32_t)__builtin_amdgcn_update_dpp(0, (int)kh, 0x130, 0xf, 0xf, false) << 32) |
-                        (uint32_t)__builtin_amdgcn_update_dpp(0, (int)kl, 0x130, 0xf, 0xf, false);
-          if (lane == 0 && j > 0) pv = stage[j - 1].key;
-          if ((lane == 63 || j + 1 == jend) && j + 1 < nvalid) nx = stage[j + 1].key;
-          const uint64_t pk = v.key & seg.pmask;
-          const bool sp = j > 0 && (pv & seg.pmask) == pk;
-          const bool sn = j + 1 < nvalid && (nx & seg.pmask) == pk;
-          if (sp || sn) {
-            // Walk the segment in LDS (bounded: kSegMax each way).  The first
-            // kSegWin neighbours each way are loaded together (independent
-            // LDS reads; segments hold ~2 records at the runtime's bytes), and
-            // the walk goes on one read at a time only past them.  Out of
-            // range, a neighbour reads as ~v.key, outside the segment.
-            uint32_t less = 0, eqb = 0;
-            const int klo = j - kSegMax > 0 ? j - kSegMax : 0;
-            const int khi = j + 1 + kSegMax < nvalid ? j + 1 + kSegMax : nvalid;
-            uint64_t wb[kSegWin > 0 ? kSegWin : 1], wf[kSegWin > 0 ? kSegWin : 1];
-#pragma unroll
-            for (int q = 0; q < kSegWin; ++q) {
-              wb[q] = j - 1 - q >= klo ? stage[j - 1 - q].key : ~v.key;
-              wf[q] = j + 1 + q < khi ? stage[j + 1 + q].key : ~v.key;
-            }
-            int k = j - 1;
-            bool on = true;
-#pragma unroll
-            for (int q = 0; q < kSegWin; ++q) {
-              on = on && (wb[q] & seg.pmask) == pk;
-              if (on) {
-                less += wb[q] < v.key ? 1u : 0u;
-                eqb += wb[q] == v.key ? 1u : 0u;
-                --k;
-              }
-            }
-            while (on && k >= klo) {
-              const uint64_t kk = stage[k].key;
-              if ((kk & seg.pmask) != pk) break;
-              less += kk < v.key ? 1u : 0u;
-              eqb += kk == v.key ? 1u : 0u;
-              --k;
-            }
-            const int sfirst = k + 1;  // the segment's first stage slot
-            // kSegMax records walked without leaving the segment: too long
-            bool too_long = k < klo && klo > 0;
-            k = j + 1;
-            on = true;
-#pragma unroll
-            for (int q = 0; q < kSegWin; ++q) {
-              on = on && (wf[q] & seg.pmask) == pk;
-              if (on) {
-                less += wf[q] < v.key ? 1u : 0u;
-                ++k;
-              }
-            }
-            while (on && k < khi) {
-              const uint64_t kk = stage[k].key;
-              if ((kk & seg.pmask) != pk) break;
-              less += kk < v.key ? 1u : 0u;
-              ++k;
-            }
-            too_long |= k == khi && khi < nvalid;
-            // 2: this tile's slots may collide (not a permutation, SegPass).
-            if (too_long) atomicOr(seg.err, 2u);
-            pos = sfirst + (int)(less + eqb);
-          }
-        }
+        if (SEG) pos = seg_pos(v, j, jend);
         const uint32_t d = (uint32_t)(v.key >> shift) & (kBuckets - 1);
         emit(skew_tag, v, j, delta[d] + pos, NEXT ? cut[d] : 0u);
         if (C16 && mixed16) {
