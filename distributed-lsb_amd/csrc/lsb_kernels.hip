@@ -927,6 +927,10 @@ __device__ unsigned long long g_os_prof[10];
 #define LSB_SEG_WIN 2
 #endif
 constexpr int kSegWin = LSB_SEG_WIN;
+// The SEG instance's stage neighbours from LDS instead of DPP (experiment).
+#ifndef LSB_SEG_LDSNB
+#define LSB_SEG_LDSNB 0
+#endif
 // The SEG instance's whole tiles through the batched write-out (records, then
 // their delta entries, read LSB_SEG_BATCH at a time first; 0: one by one).
 #ifndef LSB_SEG_BATCH
@@ -1430,6 +1434,12 @@ __device__ __forceinline__ void onesweep_body(
     // hold consecutive j, so the neighbours are the next lanes (DPP).
     auto seg_pos = [&](const Elem& v, int j, int jend) -> int {
       int pos = j;
+#if LSB_SEG_LDSNB
+      // Stage neighbours j - 1 and j + 1 read from LDS by every lane (two
+      // independent reads; no DPP, no edge-lane branches).
+      const uint64_t pv = j > 0 ? stage[j - 1].key : ~v.key;
+      const uint64_t nx = j + 1 < nvalid ? stage[j + 1].key : ~v.key;
+#else
       // Stage neighbours j - 1 and j + 1 are the neighbouring lanes'
       // records (the wave's j are consecutive; lanes 0 and 63 read LDS).
       const uint32_t kl = (uint32_t)v.key, kh = (uint32_t)(v.key >> 32);
@@ -1439,6 +1449,7 @@ __device__ __forceinline__ void onesweep_body(
                     (uint32_t)__builtin_amdgcn_update_dpp(0, (int)kl, 0x130, 0xf, 0xf, false);
       if (lane == 0 && j > 0) pv = stage[j - 1].key;
       if ((lane == 63 || j + 1 == jend) && j + 1 < nvalid) nx = stage[j + 1].key;
+#endif
       const uint64_t pk = v.key & seg.pmask;
       const bool sp = j > 0 && (pv & seg.pmask) == pk;
       const bool sn = j + 1 < nvalid && (nx & seg.pmask) == pk;
@@ -1454,8 +1465,9 @@ __device__ __forceinline__ void onesweep_body(
         uint64_t wb[kSegWin > 0 ? kSegWin : 1], wf[kSegWin > 0 ? kSegWin : 1];
 #pragma unroll
         for (int q = 0; q < kSegWin; ++q) {
-          wb[q] = j - 1 - q >= klo ? stage[j - 1 - q].key : ~v.key;
-          wf[q] = j + 1 + q < khi ? stage[j + 1 + q].key : ~v.key;
+          // (the first of each: pv / nx, already read)
+          wb[q] = q == 0 && j - 1 >= klo ? pv : j - 1 - q >= klo ? stage[j - 1 - q].key : ~v.key;
+          wf[q] = q == 0 && j + 1 < khi ? nx : j + 1 + q < khi ? stage[j + 1 + q].key : ~v.key;
         }
         int k = j - 1;
         bool on = true;

@@ -128,17 +128,20 @@ def test_world_of_one_rccl_every_record_through_the_collective(lsb_built, oracle
             w.close()
 
 
-@pytest.mark.parametrize("world,extra", [(2, {}), (4, {}), (8, {}), (2, {"LSB_RCCL_CALL_U64": "4096"})])
-def test_real_rccl_ranks(lsb_built, world, extra):
+@pytest.mark.parametrize("world,extra,exchange", [(2, {}, "alltoallv"), (4, {}, "alltoallv"), (8, {}, "alltoallv"),
+                                                  (2, {"LSB_RCCL_CALL_U64": "4096"}, "alltoallv"),
+                                                  (4, {}, "p2p")])
+def test_real_rccl_ranks(lsb_built, world, extra, exchange):
     """Real RCCL ranks (one process each, socket transport on the one GPU,
     tools/rccl_two_ranks.py) with LSB_EXCHANGE_CHUNKS=8: the golden digest
     and every rank verified; with a small call bound the chunks' calls are
-    cut too."""
+    cut too; grouped ncclSend / ncclRecv (LSB_OPT_EXCHANGE_P2P) on the wire
+    stream as well."""
     import json
     n = {2: 1_000_000, 4: 1_000_003, 8: 1_048_576}[world]
     env = dict(os.environ, LSB_EXCHANGE_CHUNKS="8", **extra)
     p = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tools", "rccl_two_ranks.py"), "16", str(n),
-                        str(world), "alltoallv", "0"], capture_output=True, text=True, timeout=240, cwd=ROOT,
+                        str(world), exchange, "0"], capture_output=True, text=True, timeout=240, cwd=ROOT,
                        env=env)
     lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
     assert lines, f"rc={p.returncode}\n{p.stdout[-2000:]}\n{p.stderr[-2000:]}"
@@ -156,3 +159,19 @@ def test_stats_file_the_chunk_passes_under_the_high_byte(lsb_built, oracle_mod):
     out, _, ks = _sort(lsb_built, a, P, 4, stats=True)
     assert np.array_equal(out, oracle_mod.stable_sort(a))
     assert ks["scatter"][0] == P * 4 * (1 + 4)  # per digit: the low pass + 4 chunk passes, on each rank
+
+
+def test_skewed_split_stage_chunks(lsb_built, oracle_mod):
+    """Keys whose low bytes are skewed take the split stage (3 workgroups per
+    CU) in the chunk passes too; hot digits make one chunk hold most of the
+    block.  Bit-exact, forced split and auto."""
+    from test_gpu_sort import _dist
+    n, P = 4 * (1 << 17) + 3, 4
+    a = _dist("hot_bucket", n, np.random.default_rng(99))
+    for split in (0, 2):
+        with lsb_built.World(n, ranks=P, radix_bits=16) as w:
+            w.set_option(lsb_built.OPT_EXCHANGE_CHUNKS, 8)
+            w.set_option(lsb_built.OPT_ONESWEEP_SPLIT, split)
+            w.scatter_global(a)
+            w.my_sort()
+            assert np.array_equal(w.gather_global(), oracle_mod.stable_sort(a)), split
