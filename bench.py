@@ -1010,10 +1010,11 @@ def main():
         "placement": dict(placement, record_alloc=os.environ.get("LSB_RECORD_ALLOC", "vmm 1 GiB pieces"),
                           basis="rank 0's A and B: built from 1 GiB VMM pieces, chosen at context creation "
                                 "among K candidate buffers (by default 4 for buffers of >= 4 GiB; "
-                                "LSB_PLACEMENT_CANDIDATES = K; candidates 0: no probe) by one timed "
-                                "k_onesweep pass between every ordered pair; ms per pass, mean "
-                                "of both directions: the kept pair, the first two allocated, the slowest "
-                                "(lsb_get_placement; DESIGN.md 4)"),
+                                "LSB_PLACEMENT_CANDIDATES = K; candidates 0: no probe), each timed once "
+                                "as the destination of a k_onesweep pass (one chain of passes, losers "
+                                "freed at once); ms per pass as a destination: the kept two (mean), "
+                                "the first two allocated (mean), the slowest (lsb_get_placement; "
+                                "DESIGN.md 0, 4)"),
         "device_memory": mem,
         "verified": verified,
         "vs_baseline_basis": "MPI mpi_lsbsort 830 M elem/s (64 nodes x 128 cores, n=2^36; BASELINE.md §1)",
