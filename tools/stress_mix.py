@@ -16,8 +16,10 @@ records or the default 2^27), and some host-made keys crowd one digit-0
 bucket of one sub-array (the regions the sample may miss, so some sorts
 overflow one and start over); each line names how the sort began.  One
 draw in three sets LSB_PLACEMENT_CANDIDATES=4 (the placement probe for the
-P = 1 buffers of >= 1 GiB, built from the drawn pieces), the others 0.  Runs
-until --seconds have passed; one line per iteration.
+P = 1 buffers of >= 1 GiB, built from the drawn pieces), the others 0; and
+three draws in five send 16-bit exchanges in 2, 4 or 8 chunks
+(LSB_OPT_EXCHANGE_CHUNKS, blocks of >= 2^16 records).  Runs until
+--seconds have passed; one line per iteration.
 
     python tools/stress_mix.py --seconds 240 --seed 1
 """
@@ -109,8 +111,11 @@ def main():
         # the placement probe: off, or 4 candidates (K set: buffers of >= 1 GiB)
         probe = rng.choice((0, 0, 4))
         os.environ["LSB_PLACEMENT_CANDIDATES"] = str(probe)
+        # the exchange in chunks (LSB_OPT_EXCHANGE_CHUNKS; 16-bit exchanges of
+        # blocks of >= 2^16 records)
+        chunks = rng.choice((0, 0, 2, 4, 8))
         desc = (f"iter {it}: n={n} P={P} bits={bits} dist={dist} split={split} hybrid={hybrid} "
-                f"gather={gather} vmm={vmm} region_min={region_min} probe={probe}")
+                f"gather={gather} vmm={vmm} region_min={region_min} probe={probe} chunks={chunks}")
         t0 = time.time()
         if a.trace:  # the configuration before the sort: a fault kills the process mid-sort
             print(f"begin {desc}", flush=True)
@@ -119,6 +124,7 @@ def main():
                 w.set_option(lsbsort.OPT_ONESWEEP_SPLIT, split)
                 w.set_option(lsbsort.OPT_HYBRID, hybrid)
                 w.set_option(lsbsort.OPT_EXCHANGE_GATHER, gather)
+                w.set_option(lsbsort.OPT_EXCHANGE_CHUNKS, chunks)
                 if host:
                     arr = crowded_keys(rng, n) if dist == "crowded" else thinned_keys(rng, n)
                     w.scatter_global(arr)
