@@ -298,12 +298,22 @@ struct Chain {
   Chain(Rank& r_, Prober& pr_, uint32_t* hist2, Elem* first) : r(r_), pr(pr_), h{hist2, hist2 + lsb::kOnesweepSubs * lsb::kBuckets}, holder(first) {
     if (pr.err == hipSuccess) pr.err = lsb::launch_subhist(first, r.here, 0, r.os_grid, h[0], nullptr, r.stream);
   }
-  double pass(Elem* dst) {
-    const int next = (shift + lsb::kDigitBits) & 63;
-    const double t = time_pass(r, pr, holder, dst, shift, next, h[cur], h[cur ^ 1]);
+  int next() const { return (shift + lsb::kDigitBits) & 63; }
+  // Times holder -> dst and leaves the chain where it was: a pass does not
+  // touch its input, so the holder still has the records (and h[cur] their
+  // histogram), and a losing candidate is freed without a pass moving the
+  // records back.
+  double attempt(Elem* dst) { return time_pass(r, pr, holder, dst, shift, next(), h[cur], h[cur ^ 1]); }
+  // Moves the chain on to dst, right after attempt(dst) (which counted dst's
+  // histogram into h[cur ^ 1]).
+  void advance(Elem* dst) {
     cur ^= 1;
-    shift = next;
+    shift = next();
     holder = dst;
+  }
+  double pass(Elem* dst) {
+    const double t = attempt(dst);
+    advance(dst);
     return t;
   }
 };
@@ -354,13 +364,14 @@ int64_t record_capacity(int64_t per, int P) {
 // before it: one k_subhist read in all): X (PCG keys) and Y first, each once
 // a destination; then every further candidate Z once (the holder of the
 // records -> Z), and whichever of the two kept buffers is the slower
-// destination is freed at once -- or Z, after one more pass moves the
-// records back into a kept buffer.  At most 2K - 1 passes (7 at K = 4; round
-// 5: 13 passes and 13 histogram reads) and three buffers live: the probe's
-// transient memory is one buffer (round 5: K - 2 at once).  Interleaved with
-// round 5's form in fresh processes, 53.65-53.92 ms per sort against
-// 53.66-53.90 (profiles/r06/probe/); a form timing every candidate twice
-// gave the same (53.66-53.86) for 0.05 s more creation time.
+// destination is freed at once (the chain moves on to Z) -- or Z, and the
+// chain stays where it was (Chain::attempt: a pass leaves its input as it
+// was, so no pass moves the records back).  K + 1 passes (5 at K = 4, one of
+// them the warm-up; round 5: 13 passes and 13 histogram reads) and three
+// buffers live: the probe's transient memory is one buffer (round 5: K - 2
+// at once).  Interleaved with round 5's form in fresh processes, 53.65-53.92
+// ms per sort against 53.66-53.90 (profiles/r06/probe/); a form timing every
+// candidate twice gave the same (53.66-53.86) for 0.05 s more creation time.
 int alloc_records(lsb_ctx* c, Rank& r) {
   const size_t per = (size_t)record_capacity(c->per, c->P);
   r.cap = (int64_t)per;
@@ -404,16 +415,16 @@ int alloc_records(lsb_ctx* c, Rank& r) {
       z = nullptr;
       break;
     }
-    const double t = ch.pass(z);  // the records are in z
+    const double t = ch.attempt(z);
     worst = std::max(worst, t);
     const int slow = better(ms[0], ms[1]) ? 1 : 0;
     if (better(t, ms[slow])) {  // z replaces the slower kept buffer
+      ch.advance(z);            // the records are in z
       rec_free(keep[slow]);
       keep[slow] = z;
       ms[slow] = t;
     } else {
-      (void)ch.pass(keep[0]);  // the records back into a kept buffer
-      rec_free(z);
+      rec_free(z);  // the records are still where they were
     }
     z = nullptr;
   }
@@ -431,8 +442,8 @@ int alloc_records(lsb_ctx* c, Rank& r) {
 
 // The third record buffer R (receive buffer of the exchanges, the hybrid's
 // third pass buffer), placed like A and B: among up to 3 candidates, the
-// fastest destination (once each, in a chain of passes between B and the
-// candidate; B is scratch whenever R is first needed: before a hybrid sort,
+// fastest destination (once each, a timed pass B -> candidate that leaves
+// the records in B; B is scratch whenever R is first needed: before a hybrid sort,
 // at an exchange before its placement), each loser freed at once (two
 // buffers live at most).  A may hold records by then and is not touched; the
 // chain counts into histograms of its own, since a sort may hold one in
@@ -458,8 +469,7 @@ int alloc_third(lsb_ctx* c, Rank& r) {
       (void)hipGetLastError();
       break;
     }
-    const double t = ch.pass(z);
-    (void)ch.pass(r.B);  // the records are in B again
+    const double t = ch.attempt(z);  // the records stay in B
     if (t < best_ms) {
       rec_free(best);
       best = z;

@@ -110,10 +110,30 @@ int join_place_timed(lsb_ctx* c, Rank& r) {
   return join_place(r);
 }
 
+// [p, p + cnt) lies inside one of rank q's record buffers.  Every device
+// copy and placement of the exchange checks its ranges on the host first, so
+// a plan gone wrong fails the sort instead of faulting the device.
+bool in_buffers(const Rank& q, const Elem* p, int64_t cnt) {
+  for (const Elem* b : {q.A, q.B, q.R})
+    if (b && cnt >= 0 && p >= b && p + cnt <= b + q.cap) return true;
+  return false;
+}
+
+int copy_range(const lsb_ctx*, Rank& dst_rank, Elem* dst, const Rank& src_rank, const Elem* src, int64_t cnt,
+               hipStream_t s) {
+  if (cnt <= 0) return LSB_OK;
+  if (!in_buffers(dst_rank, dst, cnt) || !in_buffers(src_rank, src, cnt))
+    return fail(LSB_ERR_STATE, "exchange copy", "range outside the record buffers");
+  HIP_TRY(hipMemcpyAsync(dst, src, (size_t)cnt * sizeof(Elem), hipMemcpyDefault, s));
+  return LSB_OK;
+}
+
 // Place one source's received range [k0, k0 + cnt) (records at src) into B.
 int place_range(lsb_ctx* c, Rank& r, int shift, int src_rank, const Elem* src, int64_t k0,
                 int64_t cnt) {
   if (cnt <= 0) return LSB_OK;
+  if (!in_buffers(r, src, cnt) || k0 < 0 || k0 + cnt > r.cap)
+    return fail(LSB_ERR_STATE, "exchange placement", "range outside the record buffers");
   // 32 algorithmic bytes per placed record, 16 per record only counted
   c->xs_place_bytes += cnt * (r.gather_next ? 16 : 32);
   (r.gather_next ? c->xs_counted : c->xs_placed) += cnt;
@@ -154,6 +174,7 @@ int place_self(lsb_ctx* c, Rank& r, int shift) {
     g.nb = c->nb;
     g.me = me;
     g.self_in_a = !(c->self_coll && c->mode != Mode::kLoopback);
+    g.a_len = g.r_len = r.cap;
     HIP_TRY(hipSetDevice(r.dev));
     Timer t(c, &r, LSB_K_EXCHANGE);
     HIP_TRY(lsb::launch_gather_desc(g, r.here, r.gdesc, r.stream));
@@ -224,8 +245,8 @@ int exchange_loopback(lsb_ctx* c, int digit) {
         const int64_t cnt = s.send_counts[q.rank];
         const int64_t lo = slice_part(cnt, j, slices_of(c)), hi = slice_part(cnt, j + 1, slices_of(c));
         if (hi <= lo) continue;
-        HIP_TRY(hipMemcpyAsync(q.R + q.recv_displs[s.rank] + lo, s.A + s.send_displs[q.rank] + lo,
-                               (size_t)(hi - lo) * sizeof(Elem), hipMemcpyDefault, q.stream));
+        LSB_TRY(copy_range(c, q, q.R + q.recv_displs[s.rank] + lo, s, s.A + s.send_displs[q.rank] + lo, hi - lo,
+                           q.stream));
       }
     }
     for (Rank& q : c->ranks) LSB_TRY(place_slice(c, q, shift, j));
@@ -666,6 +687,7 @@ int exchange_chunked(lsb_ctx* c, int digit, const std::vector<const uint32_t*>& 
     g.nb = c->nb;
     g.me = me;
     g.self_in_a = !self_in_r;
+    g.a_len = g.r_len = r.cap;
     HIP_TRY(hipSetDevice(r.dev));
     Timer t(c, &r, LSB_K_EXCHANGE);
     HIP_TRY(lsb::launch_gather_desc(g, r.here, r.gdesc, r.stream));
@@ -729,8 +751,8 @@ int exchange_chunked(lsb_ctx* c, int digit, const std::vector<const uint32_t*>& 
             const int64_t cnt = geo[q].recv[s * C + k];
             if (cnt <= 0) continue;
             const Elem* src = Y[s] + geo[s].lo[k] + geo[s].sdisp[q * C + k];
-            HIP_TRY(hipMemcpyAsync(rq.R + rq.recv_displs[s] + geo[q].rpre[s * C + k], src, (size_t)cnt * sizeof(Elem),
-                                   hipMemcpyDefault, rq.xstream));
+            LSB_TRY(copy_range(c, rq, rq.R + rq.recv_displs[s] + geo[q].rpre[s * C + k], c->ranks[s], src, cnt,
+                               rq.xstream));
           }
         }
         HIP_TRY(hipEventRecord(rq.ck_wire[k], rq.xstream));

@@ -177,6 +177,7 @@ struct GatherSrc {
   const int64_t* gadj = nullptr;    // P * nb scratch: 2 * pointer adjustment + (1: in A)
   const TileDesc* desc = nullptr;   // onesweep_tiles(m)
   int P = 1, nb = 256, me = 0, self_in_a = 1;
+  int64_t a_len = 0, r_len = 0;     // records in A and R (debug builds check every gathered read)
 };
 // gadj, then desc[t] for every onesweep tile of m records (after launch_plan
 // with gstart).

@@ -643,6 +643,12 @@ __device__ __forceinline__ const Elem* gather_search(const GatherSrc& g, int e0,
   const int64_t v = g.gadj[gather_piece(g, e0, e1, p)];
   return ((v & 1) ? g.A : g.R) + (p + (v >> 1));
 }
+#ifdef LSB_DEBUG
+// A gathered read lies inside A or R (LSB_DASSERT: debug builds only).
+__device__ __forceinline__ bool gather_in(const GatherSrc& g, const Elem* p) {
+  return (p >= g.A && p < g.A + g.a_len) || (p >= g.R && p < g.R + g.r_len);
+}
+#endif
 
 // sub_first_tile, sub_of_tile: lsb_device.h
 
@@ -1179,6 +1185,7 @@ __device__ __forceinline__ void onesweep_body(
 #pragma unroll
             for (int k = 1; k < kDescPieces; ++k) src = li >= st[k] ? pb[k] : src;
           }
+          LSB_DASSERT(li >= nvalid || gather_in(gs, src + li));
           e[i] = li < nvalid ? load_elem_nt(src + li) : Elem{0ull, 0ull};
         }
       } else {
@@ -1188,6 +1195,7 @@ __device__ __forceinline__ void onesweep_body(
 #pragma unroll
         for (int i = 0; i < IPT; ++i) {
           const int li = wbase + i * 64;
+          LSB_DASSERT(li >= nvalid || gather_in(gs, gather_search(gs, e0, e1, tb + li)));
           e[i] = li < nvalid ? load_elem_nt(gather_search(gs, e0, e1, tb + li)) : Elem{0ull, 0ull};
           __builtin_amdgcn_sched_barrier(0);
         }

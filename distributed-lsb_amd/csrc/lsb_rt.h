@@ -422,6 +422,11 @@ int ensure_recv(lsb_ctx* c, Rank& r);
 int join_place(Rank& r);
 int join_place_timed(lsb_ctx* c, Rank& r);
 int exchange_digit(lsb_ctx* c, int digit);
+// A loopback exchange's device copy of cnt records src (a record buffer of
+// src_rank) -> dst (one of dst_rank's), checked against the buffers first.
+bool in_buffers(const Rank& q, const Elem* p, int64_t cnt);
+int copy_range(const lsb_ctx* c, Rank& dst_rank, Elem* dst, const Rank& src_rank, const Elem* src, int64_t cnt,
+               hipStream_t s);
 // The per-digit exchange in chunks: digit `digit` (16 bits) whose low-byte
 // pass has run (A sorted by the low byte; lo_hist its input's sub-array
 // histogram on each rank), high-byte passes chunk by chunk, each chunk's

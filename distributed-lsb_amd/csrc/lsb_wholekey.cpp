@@ -285,8 +285,8 @@ int exchange_merge(lsb_ctx* c) {
         slice_runs(c, q, g, j, sr, &lo, &hi);
         for (Rank& s : c->ranks) {
           if (s.rank == q.rank || sr[s.rank].len == 0) continue;
-          HIP_TRY(hipMemcpyAsync(q.R + sr[s.rank].roff, s.A + q.mcut[s.rank * K1 + (size_t)q.rank * g.S + j],
-                                 (size_t)sr[s.rank].len * sizeof(Elem), hipMemcpyDefault, q.stream));
+          LSB_TRY(copy_range(c, q, q.R + sr[s.rank].roff, s, s.A + q.mcut[s.rank * K1 + (size_t)q.rank * g.S + j],
+                             sr[s.rank].len, q.stream));
         }
       }
       for (Rank& q : c->ranks) LSB_TRY(merge_slice_async(c, q, g, j, final_b ? q.B : q.R));

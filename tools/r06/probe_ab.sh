@@ -4,12 +4,13 @@
 # of 4 candidates): bench.py at N = 1 in fresh processes, alternated.  The
 # round-5 library is built from git revision 860dbc9 by tools/build_at.sh
 # into distributed-lsb_amd/build/ab_r05; r06a (one timed pass per candidate,
-# a histogram read before each) from commit 1220170 into build/ab_r06a.
+# a histogram read before each) from commit 1220170 into build/ab_r06a;
+# head: the last commit (FORMS="head r06": a working-tree change against it).
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R
 O=$R/gpurun_out/${TAG:-r06_probe}; mkdir -p $O
 declare -A LIB=([r05]=$R/distributed-lsb_amd/build/ab_r05/liblsb.so [r06]=$R/distributed-lsb_amd/build/liblsb.so
-               [r06a]=$R/distributed-lsb_amd/build/ab_r06a/liblsb.so)
+               [r06a]=$R/distributed-lsb_amd/build/ab_r06a/liblsb.so [head]=$R/distributed-lsb_amd/build/ab_head/liblsb.so)
 F=${FORMS:-"r05 r06"}
 for k in $(seq 1 ${ROUNDS:-4}); do
   list=$F; [ $((k % 2)) = 0 ] && list=$(echo $F | tr ' ' '\n' | tac | tr '\n' ' ')

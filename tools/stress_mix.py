@@ -84,11 +84,15 @@ def main():
                     help="share of iterations that sort host-made (thinned / crowded) keys")
     ap.add_argument("--hybrid", type=int, choices=(0, 1, 2), default=None,
                     help="force LSB_OPT_HYBRID instead of drawing it (the draw still happens)")
+    ap.add_argument("--draws", choices=("current", "r05", "r05v12"), default="current",
+                    help="an earlier round's draws (as tools/stress_replay.py): r05v12 without the probe and "
+                         "chunk draws, r05 without the chunk draw")
+    ap.add_argument("--iters", type=int, default=0, help="stop after this many sorts (0: --seconds only)")
     a = ap.parse_args()
     rng = random.Random(a.seed)
     t_end = time.time() + a.seconds
     it = bad = 0
-    while time.time() < t_end:
+    while time.time() < t_end and (a.iters <= 0 or it < a.iters):
         n = int(2 ** rng.uniform(0, a.max_log2)) + rng.randrange(0, 4096)
         P = rng.choice((1, 1, 2, 3, 8))
         bits = rng.choice((8, 16, 64))
@@ -109,11 +113,11 @@ def main():
         vmm = rng.choice((2, 64, 1024, 1024))
         os.environ["LSB_VMM_CHUNK_MIB"] = str(vmm)
         # the placement probe: off, or 4 candidates (K set: buffers of >= 1 GiB)
-        probe = rng.choice((0, 0, 4))
+        probe = rng.choice((0, 0, 4)) if a.draws != "r05v12" else 0
         os.environ["LSB_PLACEMENT_CANDIDATES"] = str(probe)
         # the exchange in chunks (LSB_OPT_EXCHANGE_CHUNKS; 16-bit exchanges of
         # blocks of >= 2^16 records)
-        chunks = rng.choice((0, 0, 2, 4, 8))
+        chunks = rng.choice((0, 0, 2, 4, 8)) if a.draws == "current" else 0
         desc = (f"iter {it}: n={n} P={P} bits={bits} dist={dist} split={split} hybrid={hybrid} "
                 f"gather={gather} vmm={vmm} region_min={region_min} probe={probe} chunks={chunks}")
         t0 = time.time()
