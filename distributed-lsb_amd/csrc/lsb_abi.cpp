@@ -340,8 +340,9 @@ int lsb_pass(lsb_ctx_t* c, int digit) {
   return do_pass(c, digit);
 }
 
-int lsb_sort(lsb_ctx_t* c) {
-  LSB_TRY(check_ctx(c));
+namespace {
+
+int sort_body(lsb_ctx* c) {
   std::vector<Timer> sort_timers;
   sort_timers.reserve(c->ranks.size());
   for (Rank& r : c->ranks) sort_timers.emplace_back(c, &r, LSB_K_SORT);
@@ -378,6 +379,28 @@ int lsb_sort(lsb_ctx_t* c) {
   }
   for (Timer& t : sort_timers) t.stop();
   return LSB_OK;
+}
+
+// A sort that failed part-way may leave work queued on a rank's placement
+// or wire stream (an exchange's placements, the chunked exchange's
+// transfers) that reads or writes the record buffers; the next call on the
+// context queues on the rank's stream only.  Wait for all of it before the
+// error goes back, so no later sort races with it.
+void quiesce(lsb_ctx* c) {
+  for (Rank& r : c->ranks) {
+    (void)hipSetDevice(r.dev);
+    for (hipStream_t s : {r.stream, r.pstream, r.xstream})
+      if (s) (void)hipStreamSynchronize(s);
+  }
+}
+
+}  // namespace
+
+int lsb_sort(lsb_ctx_t* c) {
+  LSB_TRY(check_ctx(c));
+  const int rc = sort_body(c);
+  if (rc != LSB_OK) quiesce(c);
+  return rc;
 }
 
 int lsb_get_last_sort(lsb_ctx_t* c, int* local_passes, int* exchanges, uint64_t* varying_bits) {

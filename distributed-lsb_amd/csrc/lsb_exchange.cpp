@@ -725,6 +725,8 @@ int exchange_chunked(lsb_ctx* c, int digit, const std::vector<const uint32_t*>& 
         x.halves = r.os_halves;
         const int grid = std::max(lsb::kOnesweepSubs, (r.os_grid - c->xchunk_reserve) / 8 * 8);
         hipError_t e;
+        if (c->fail_onesweep > 0 && --c->fail_onesweep == 0)  // LSB_OPT_FAIL_ONESWEEP (tests)
+          return fail(LSB_ERR_HIP, "exchange_chunked: launch_onesweep", "injected launch failure (LSB_OPT_FAIL_ONESWEEP)");
         {
           Timer t(c, &r, LSB_K_SCATTER);
           e = lsb::launch_onesweep(X[i] + lo, Y[i] + lo, m, hi_shift, -1,

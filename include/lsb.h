@@ -132,10 +132,14 @@ typedef struct lsb_ctx lsb_ctx_t;
                                       16 B of writes per record) before it; 0 places every
                                       exchange.  Same output. */
 #define LSB_OPT_FAIL_ONESWEEP   11 /* tests (fault injection): n >= 1 makes the n-th k_onesweep
-                                      launch from now fail with LSB_ERR_HIP before it is queued,
-                                      as a failed launch would; 0 (default) off.  The context
-                                      stays usable: its buffers keep their roles and the next
-                                      sort starts from the input still in A. */
+                                      launch from now (the chunked exchange's chunk passes
+                                      included) fail with LSB_ERR_HIP before it is queued, as a
+                                      failed launch would; 0 (default) off.  The context stays
+                                      usable: its buffers keep their roles and the next sort
+                                      starts from the records in A (the input, or after an
+                                      exchange's local pass a permutation of it).  lsb_sort
+                                      returns any error only once every rank's streams are
+                                      idle. */
 #define LSB_OPT_REGION_FIRST    12 /* P == 1 sorts of >= 2^27 records by the LSD passes:
                                       1 (default) the first pass takes no histogram read: it
                                       writes each (digit, sub-array) class of records into a

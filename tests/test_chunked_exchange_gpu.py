@@ -175,3 +175,29 @@ def test_skewed_split_stage_chunks(lsb_built, oracle_mod):
             w.scatter_global(a)
             w.my_sort()
             assert np.array_equal(w.gather_global(), oracle_mod.stable_sort(a)), split
+
+
+def test_failed_chunk_pass_then_sort(lsb_built, oracle_mod):
+    """A chunk pass that fails to launch (LSB_OPT_FAIL_ONESWEEP) after earlier
+    chunks' transfers were queued on the wire streams: lsb_sort waits for
+    every rank's streams before it reports the error (quiesce), A still holds
+    a permutation of the records (the low-byte pass's output), and the next
+    sort on the same context sorts it exactly."""
+    L = lsb_built
+    n, P = 4 * (1 << 17) + 3, 4
+    with L.World(n, ranks=P, radix_bits=16) as w:
+        w.set_option(L.OPT_EXCHANGE_CHUNKS, 8)
+        w.generate()
+        inp = w.gather_global()
+        # 4 low-byte passes (one per rank), then chunk passes rank by rank:
+        # the 14th launch is chunk 2 of rank 1, after chunks 0 and 1 went out.
+        w.set_option(L.OPT_FAIL_ONESWEEP, 14)
+        with pytest.raises(L.LsbError):
+            w.my_sort()
+        w.set_option(L.OPT_FAIL_ONESWEEP, 0)
+        held = w.gather_global()
+        assert np.array_equal(np.sort(held, order=["key", "val"]), np.sort(inp, order=["key", "val"]))
+        w.my_sort()
+        assert np.array_equal(w.gather_global(), oracle_mod.stable_sort(held))
+        assert w.verify() == (True, -1)
+        assert w.check_sorted()
