@@ -332,12 +332,31 @@ int lsb_copy_out(lsb_ctx_t* c, int rank, int64_t off, int64_t cnt, lsb_elem_t* h
   return LSB_OK;
 }
 
+namespace {
+
+// A sort that failed part-way may leave work queued on a rank's placement
+// or wire stream (an exchange's placements, the chunked exchange's
+// transfers) that reads or writes the record buffers; the next call on the
+// context queues on the rank's stream only.  Wait for all of it before the
+// error goes back, so no later sort races with it.
+void quiesce(lsb_ctx* c) {
+  for (Rank& r : c->ranks) {
+    (void)hipSetDevice(r.dev);
+    for (hipStream_t s : {r.stream, r.pstream, r.xstream})
+      if (s) (void)hipStreamSynchronize(s);
+  }
+}
+
+}  // namespace
+
 int lsb_pass(lsb_ctx_t* c, int digit) {
   LSB_TRY(check_ctx(c));
   if (digit < 0 || digit >= 64 / c->bits) return fail(LSB_ERR_INVALID, "lsb_pass", "digit");
   // Filed under the digit's own local passes (a 64-bit digit: the whole sort).
   c->pass_cursor = c->bits == 64 ? 0 : digit * (c->bits / lsb::kDigitBits);
-  return do_pass(c, digit);
+  const int rc = do_pass(c, digit);
+  if (rc != LSB_OK) quiesce(c);
+  return rc;
 }
 
 namespace {
@@ -379,19 +398,6 @@ int sort_body(lsb_ctx* c) {
   }
   for (Timer& t : sort_timers) t.stop();
   return LSB_OK;
-}
-
-// A sort that failed part-way may leave work queued on a rank's placement
-// or wire stream (an exchange's placements, the chunked exchange's
-// transfers) that reads or writes the record buffers; the next call on the
-// context queues on the rank's stream only.  Wait for all of it before the
-// error goes back, so no later sort races with it.
-void quiesce(lsb_ctx* c) {
-  for (Rank& r : c->ranks) {
-    (void)hipSetDevice(r.dev);
-    for (hipStream_t s : {r.stream, r.pstream, r.xstream})
-      if (s) (void)hipStreamSynchronize(s);
-  }
 }
 
 }  // namespace
