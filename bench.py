@@ -585,8 +585,9 @@ def extra_timeout(a):
 
 def extras_at(a, N):
     """The extra forms timed after the headline, in fresh processes: (name,
-    argv).  N > 1: the whole-key exchange and the peer-store exchange (unless
-    the headline already is that form); N = 1: the hybrid local sort."""
+    argv).  N > 1: the whole-key exchange, the chunked 16-bit exchange and
+    the peer-store exchange (unless the headline already is that form);
+    N = 1: the hybrid local sort and the forced 16-bit exchange (x16)."""
     if a.no_extras:
         return []
     radix = a.radix_bits or (8 if N == 1 else 16)
@@ -600,12 +601,15 @@ def extras_at(a, N):
     out = []
     if radix != 64 and not a.no_whole_key:
         out.append(("whole_key", whole_key_argv(a)))
-    if radix != 64 and a.exchange != "peer" and not a.no_peer and a.transport != "gloo":
-        out.append(("peer", peer_argv(a)))
     # the 16-bit exchange in chunks (LSB_OPT_EXCHANGE_CHUNKS = 8): each chunk's
     # records on the wire while the next chunk's high-byte pass runs
     if radix == 16 and a.exchange == "alltoallv" and not a.exchange_chunks and a.transport != "gloo":
         out.append(("chunked", extra_argv(a, ["--exchange-chunks", "8"])))
+    # last: the only form whose kernels store into another GPU's memory (IPC
+    # mappings), never run across devices before; whatever it does to the
+    # node, the other forms have been measured
+    if radix != 64 and a.exchange != "peer" and not a.no_peer and a.transport != "gloo":
+        out.append(("peer", peer_argv(a)))
     return out
 
 
