@@ -73,6 +73,57 @@ def crowded_keys(rng, n):
     return a
 
 
+def draw(rng, max_log2, draws="current", host_share=1 / 3, force_hybrid=None):
+    """One iteration's configuration, drawn in a fixed order (tools/stress_replay.py
+    replays the sequence without sorting).  draws: "current", or an earlier
+    round's sequence -- "r05v12" (round 5's run v12: no probe and no chunk
+    draws), "r05" (no chunk draw).  Host-made keys are drawn afterwards by
+    host_keys, from the same rng."""
+    n = int(2 ** rng.uniform(0, max_log2)) + rng.randrange(0, 4096)
+    P = rng.choice((1, 1, 2, 3, 8))
+    bits = rng.choice((8, 16, 64))
+    dist = rng.choice(("uniform", "zipf"))
+    split = rng.choice((0, 1, 2))
+    hybrid = rng.choice((0, 1, 1, 2))
+    gather = rng.choice((0, 1, 1))  # LSB_OPT_EXCHANGE_GATHER (per-digit exchange forms)
+    if force_hybrid is not None:
+        hybrid = force_hybrid
+    host = rng.random() < host_share
+    if host:
+        n = min(n, 1 << 22)
+        dist = "crowded" if rng.random() < 0.25 else "thinned"
+    region_min = rng.choice((1 << 16, 1 << 27))
+    # record buffers from VMM pieces of 2 / 64 MiB (several pieces per
+    # buffer at these sizes), or the default 1 GiB (hipMalloc below it)
+    vmm = rng.choice((2, 64, 1024, 1024))
+    # the placement probe: off, or 4 candidates (K set: buffers of >= 1 GiB)
+    probe = rng.choice((0, 0, 4)) if draws != "r05v12" else 0
+    # the exchange in chunks (LSB_OPT_EXCHANGE_CHUNKS; 16-bit exchanges of
+    # blocks of >= 2^16 records)
+    chunks = rng.choice((0, 0, 2, 4, 8)) if draws == "current" else 0
+    return dict(n=n, P=P, bits=bits, dist=dist, split=split, hybrid=hybrid, gather=gather, host=host,
+                region_min=region_min, vmm=vmm, probe=probe, chunks=chunks)
+
+
+def host_keys(rng, cfg):
+    """The host-made keys of a configuration with cfg["host"]."""
+    return crowded_keys(rng, cfg["n"]) if cfg["dist"] == "crowded" else thinned_keys(rng, cfg["n"])
+
+
+def set_env(cfg):
+    """The configuration's environment knobs, read at context creation."""
+    os.environ["LSB_REGION_MIN"] = str(cfg["region_min"])
+    os.environ["LSB_VMM_CHUNK_MIB"] = str(cfg["vmm"])
+    os.environ["LSB_PLACEMENT_CANDIDATES"] = str(cfg["probe"])
+
+
+def set_options(w, cfg):
+    w.set_option(lsbsort.OPT_ONESWEEP_SPLIT, cfg["split"])
+    w.set_option(lsbsort.OPT_HYBRID, cfg["hybrid"])
+    w.set_option(lsbsort.OPT_EXCHANGE_GATHER, cfg["gather"])
+    w.set_option(lsbsort.OPT_EXCHANGE_CHUNKS, cfg["chunks"])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=240)
@@ -93,44 +144,20 @@ def main():
     t_end = time.time() + a.seconds
     it = bad = 0
     while time.time() < t_end and (a.iters <= 0 or it < a.iters):
-        n = int(2 ** rng.uniform(0, a.max_log2)) + rng.randrange(0, 4096)
-        P = rng.choice((1, 1, 2, 3, 8))
-        bits = rng.choice((8, 16, 64))
-        dist = rng.choice(("uniform", "zipf"))
-        split = rng.choice((0, 1, 2))
-        hybrid = rng.choice((0, 1, 1, 2))
-        gather = rng.choice((0, 1, 1))  # LSB_OPT_EXCHANGE_GATHER (per-digit exchange forms)
-        if a.hybrid is not None:
-            hybrid = a.hybrid
-        host = rng.random() < a.host_share
-        if host:
-            n = min(n, 1 << 22)
-            dist = "crowded" if rng.random() < 0.25 else "thinned"
-        region_min = rng.choice((1 << 16, 1 << 27))
-        os.environ["LSB_REGION_MIN"] = str(region_min)
-        # record buffers from VMM pieces of 2 / 64 MiB (several pieces per
-        # buffer at these sizes), or the default 1 GiB (hipMalloc below it)
-        vmm = rng.choice((2, 64, 1024, 1024))
-        os.environ["LSB_VMM_CHUNK_MIB"] = str(vmm)
-        # the placement probe: off, or 4 candidates (K set: buffers of >= 1 GiB)
-        probe = rng.choice((0, 0, 4)) if a.draws != "r05v12" else 0
-        os.environ["LSB_PLACEMENT_CANDIDATES"] = str(probe)
-        # the exchange in chunks (LSB_OPT_EXCHANGE_CHUNKS; 16-bit exchanges of
-        # blocks of >= 2^16 records)
-        chunks = rng.choice((0, 0, 2, 4, 8)) if a.draws == "current" else 0
-        desc = (f"iter {it}: n={n} P={P} bits={bits} dist={dist} split={split} hybrid={hybrid} "
-                f"gather={gather} vmm={vmm} region_min={region_min} probe={probe} chunks={chunks}")
+        cfg = draw(rng, a.max_log2, a.draws, a.host_share, a.hybrid)
+        set_env(cfg)
+        n, P, bits, dist = cfg["n"], cfg["P"], cfg["bits"], cfg["dist"]
+        desc = (f"iter {it}: n={n} P={P} bits={bits} dist={dist} split={cfg['split']} hybrid={cfg['hybrid']} "
+                f"gather={cfg['gather']} vmm={cfg['vmm']} region_min={cfg['region_min']} probe={cfg['probe']} "
+                f"chunks={cfg['chunks']}")
         t0 = time.time()
         if a.trace:  # the configuration before the sort: a fault kills the process mid-sort
             print(f"begin {desc}", flush=True)
         try:
             with lsbsort.World(n, ranks=P, radix_bits=bits) as w:
-                w.set_option(lsbsort.OPT_ONESWEEP_SPLIT, split)
-                w.set_option(lsbsort.OPT_HYBRID, hybrid)
-                w.set_option(lsbsort.OPT_EXCHANGE_GATHER, gather)
-                w.set_option(lsbsort.OPT_EXCHANGE_CHUNKS, chunks)
-                if host:
-                    arr = crowded_keys(rng, n) if dist == "crowded" else thinned_keys(rng, n)
+                set_options(w, cfg)
+                if cfg["host"]:
+                    arr = host_keys(rng, cfg)
                     w.scatter_global(arr)
                     w.my_sort()
                     got = w.gather_global()
