@@ -201,3 +201,36 @@ def test_failed_chunk_pass_then_sort(lsb_built, oracle_mod):
         assert np.array_equal(w.gather_global(), oracle_mod.stable_sort(held))
         assert w.verify() == (True, -1)
         assert w.check_sorted()
+
+
+@pytest.mark.parametrize("n,P,chunks", [(4 * 65536, 4, 8),          # per = 2^16 exactly: chunked
+                                        (4 * 65536 - 4, 4, 8),      # per just below: unchunked
+                                        (3 * 65536 + 1, 3, 4),      # ragged: the last rank is 2 short
+                                        (8 * 70000 + 7, 8, 2)])
+def test_block_sizes_at_the_threshold(lsb_built, oracle_mod, n, P, chunks):
+    """Blocks at the chunking threshold (kChunkMinPer = 2^16 records per
+    rank) and ragged last ranks: bit-exact either way, same local passes and
+    exchanges as the unchunked sort."""
+    a = _uniform(n, n + P)
+    out, last, _ = _sort(lsb_built, a, P, chunks)
+    assert np.array_equal(out, oracle_mod.stable_sort(a))
+    _, last0, _ = _sort(lsb_built, a, P, 0)
+    assert last == last0
+
+
+@pytest.mark.parametrize("form", ["first", "ends", "middle"])
+def test_empty_chunks(lsb_built, oracle_mod, form):
+    """The low byte of every digit limited so that at C = 8 (32 values per
+    chunk) most chunks are empty on every rank (no pass, empty transfers):
+    only chunk 0 ("first"), chunks 0 and 7 ("ends"), chunks 2 and 3
+    ("middle")."""
+    n, P = 4 * (1 << 17) + 11, 4
+    a = _uniform(n, 40 + len(form))
+    rng = np.random.default_rng(len(form))
+    pool = {"first": np.arange(0, 32), "ends": np.array([0, 1, 254, 255]), "middle": np.arange(64, 128)}[form]
+    for d in range(4):
+        sh = np.uint64(16 * d)
+        lo = pool[rng.integers(0, pool.size, n)].astype(np.uint64)
+        a["key"] = (a["key"] & ~(np.uint64(0xFF) << sh)) | (lo << sh)
+    out, _, _ = _sort(lsb_built, a, P, 8)
+    assert np.array_equal(out, oracle_mod.stable_sort(a))
