@@ -2,8 +2,8 @@
 # A/B of the gathered pass's write-out / descriptor variants:
 # tools/r06/gather_probe.py's gathered form (16-bit, exchange forced at P = 1,
 # 2^30) per build, in fresh processes, the build order alternating per round.
-# The variants were compile-time flags of lsb_kernels.hip at commit 606426e's
-# parent (LSB_GATHER_BATCH, LSB_GATHER_EARLY_DESC, LSB_GATHER_LANESEL,
+# The variants were compile-time flags of lsb_kernels.hip in the working tree
+# before commit ba33369, never committed (LSB_GATHER_BATCH, LSB_GATHER_EARLY_DESC, LSB_GATHER_LANESEL,
 # LSB_GATHER_SDESC, LSB_GATHER_PF, LSB_GRAB_ASYNC; built by
 # tools/build_variant.sh into build/ab_g_*); the shipped form is SDESC + PF 64,
 # and LSB_GATHER_IDENTITY (build/ab_g_id) is still there.  Results:
