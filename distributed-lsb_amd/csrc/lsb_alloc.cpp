@@ -5,6 +5,7 @@
 // candidate buffers (LSB_PLACEMENT_CANDIDATES).  DESIGN.md §4.
 #include "lsb_rt.h"
 
+#include <atomic>
 #include <mutex>
 
 namespace lsb_rt {
@@ -52,7 +53,35 @@ void vmm_release(VmmBuffer& b, size_t piece) {
   b = VmmBuffer();
 }
 
+// RCCL and VMM address reuse.  RCCL 2.27.7 over VMM record buffers mapped at
+// addresses that an earlier RCCL context's (released) VMM buffers had used
+// delivered garbage: a world-of-one context sorting 2^28 records with 8-bit
+// digits through ncclAllToAllv failed lsb_verify from its process's third
+// such context on (zeros at the head, records lost; 3 of 5 and 3 of 6 sorts),
+// never with hipMalloc'd buffers (5 of 5), nor while released address ranges
+// stayed reserved (6 of 6, but then their memory is not given back: 288 ->
+// 147 GiB free after 4 contexts); the reservation's address hint is not
+// honoured, so the runtime hands the same ranges out again.
+// profiles/r06/large_call/, tests/test_gpu_sort.py
+// test_world_of_one_large_calls.  So once a VMM buffer of an
+// RCCL context has been released in this process, later RCCL contexts take
+// hipMalloc'd record buffers.  A process's first RCCL context keeps VMM
+// pieces: every address RCCL sees there is mapped once (the placement
+// probe's candidates are released before any collective touches them), so
+// the bench's ranks (one context per process) are unchanged.
+// LSB_RCCL_VMM=1 keeps VMM pieces regardless (reproduction).
+std::atomic<bool> g_rccl_vmm_released{false};
+
+bool malloc_for(const lsb_ctx* c) {
+  if (!c || c->mode != Mode::kRccl || !g_rccl_vmm_released.load()) return false;
+  const char* e = getenv("LSB_RCCL_VMM");
+  return !(e && atoi(e));
+}
+
 }  // namespace
+
+void mark_rccl_vmm_released() { g_rccl_vmm_released.store(true); }
+
 
 size_t rec_bytes(size_t count) {
   const size_t piece = vmm_piece_bytes();
@@ -72,7 +101,7 @@ bool rec_is_vmm(const void* p) {
 // (piece j of every buffer before piece j + 1 of any).
 int rec_alloc_group(const lsb_ctx* c, Elem** const* outs, int k, size_t count) {
   for (int i = 0; i < k; ++i) *outs[i] = nullptr;
-  const size_t piece = vmm_piece_bytes();
+  const size_t piece = malloc_for(c) ? 0 : vmm_piece_bytes();
   const size_t want = std::max<size_t>(count, 1) * sizeof(Elem);
   if (piece == 0 || want < piece) {
     for (int i = 0; i < k; ++i) {

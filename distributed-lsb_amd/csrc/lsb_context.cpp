@@ -157,6 +157,11 @@ void free_rank(Rank& r, const lsb_ctx* c) {
 #else
   (void)c;
 #endif
+  // RCCL has seen this context's record buffers: VMM ones released here make
+  // later RCCL contexts of the process take hipMalloc'd ones (lsb_alloc.cpp).
+  if (c && c->mode == Mode::kRccl)
+    for (const Elem* p : {r.A, r.B, r.R})
+      if (p && rec_is_vmm(p)) mark_rccl_vmm_released();
   for (void* p : r.ipc_opened) (void)hipIpcCloseMemHandle(p);
   (void)hipFree(r.peer_base);
   (void)hipFree(r.split_state);

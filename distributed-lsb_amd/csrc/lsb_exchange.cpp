@@ -314,6 +314,7 @@ int peer_setup(lsb_ctx* c) {
     for (Elem** p : {&r.A, &r.B, &r.R})
       if (*p == old) *p = nu;
     r.buf[k] = nu;
+    if (c->mode == Mode::kRccl) mark_rccl_vmm_released();
     rec_free(old);
   }
   static_assert(sizeof(hipIpcMemHandle_t) % 8 == 0, "handle in u64 words");

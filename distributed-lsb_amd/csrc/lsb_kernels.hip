@@ -942,17 +942,12 @@ constexpr int kSegWin = LSB_SEG_WIN;
 #ifndef LSB_SEG_BATCH
 #define LSB_SEG_BATCH 4
 #endif
-// GATHER: each wave reads its tile's descriptor (TileDesc) itself right
-// after the loop-top barrier, by scalar loads, and one lane loads the
-// descriptor LSB_GATHER_PF tiles ahead in the sub-array into L2 for the
-// workgroup that will take that tile.  Until round 6 wave 0 fetched the next
-// tile's descriptor after its write-out and handed it over through LDS at
-// the loop top: waiting for that load (and a spilled LDS address reloaded
-// from scratch) meant waiting for all of wave 0's stores (vmcnt(0)) while
-// the workgroup stood at the barrier.  A gathered pass at P = 1 (2^30,
-// 16-bit, exchange forced) went 7.59-7.71 -> 7.18-7.20 ms; plain loads in
-// the same place (LSB_GATHER_IDENTITY, valid only there) 6.77-6.95
-// (profiles/r06/gather/).
+// GATHER: one lane loads the descriptor LSB_GATHER_PF tiles ahead in the
+// sub-array into L2, so wave 0's descriptor fetch for the workgroup that
+// takes that tile finds it there (0: none).  Wave 0 fetches the next tile's
+// descriptor after its write-out, so the loop top's wait for it also waits
+// for its stores (vmcnt(0)); from L2 that wait is shorter: gathered pass
+// 7.63-7.67 -> 7.45-7.48 ms at 2^30 (profiles/r06/gather/).
 #ifndef LSB_GATHER_PF
 #define LSB_GATHER_PF 64
 #endif
@@ -1011,6 +1006,7 @@ __device__ __forceinline__ void onesweep_body(
   __shared__ uint32_t scan32[W];
   __shared__ int32_t s_tile, s_sub;
   __shared__ uint32_t tile_lo[2];  // C16: low byte of the tile's first, last record
+  __shared__ TileDesc s_desc;      // GATHER: where this tile's records are
 
   const int t = threadIdx.x;
   const bool bkt = BLOCK == kBuckets || t < kBuckets;  // a bucket thread
@@ -1102,11 +1098,28 @@ __device__ __forceinline__ void onesweep_body(
   // behind this tile's write-out (computing the valid count right away made
   // wave 0, and with it the workgroup's closing barrier, wait for it).
   if (t == 0) grab(nxt_tile, nxt_sub);
+  // GATHER: lanes 0-3 of wave 0 hold the next tile's descriptor.
+  uint4 dreg = make_uint4(0u, 0u, 0u, 0u);
+  auto fetch_desc = [&]() {
+    if (GATHER && w == 0) {
+      const int nt = __builtin_amdgcn_readfirstlane(nxt_tile);
+      if (nt >= 0 && lane < 4) dreg = reinterpret_cast<const uint4*>(gs.desc + nt)[lane];
+    }
+  };
+  fetch_desc();
 
   for (;;) {
     if (t == 0) {
       s_tile = nxt_tile;
       s_sub = nxt_sub;
+    }
+    if (GATHER && w == 0 && lane < 4) {
+      // The lane's slot recomputed here, opaque to the compiler: hoisted out
+      // of the loop, it was spilled, and the spill's reload from scratch is
+      // one more memory round trip before this barrier.
+      uint32_t l;
+      asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0" : "=v"(l));
+      *reinterpret_cast<uint4*>(reinterpret_cast<char*>(&s_desc) + l * 16u) = dreg;
     }
 #pragma unroll
     for (int j = 0; j < kBuckets / 64; ++j) wcnt[w][lane + 64 * j] = 0;
@@ -1149,48 +1162,21 @@ __device__ __forceinline__ void onesweep_body(
     Elem e[IPT];
     const int wbase = w * 64 * IPT + (int)lane;
     if (GATHER) {
-      // The tile's descriptor: a uniform address in the constant address
-      // space, so scalar loads, waited on by lgkmcnt (not behind the stores).
-      typedef const __attribute__((address_space(4))) TileDesc ConstDesc;  // read-only here: s_load
-      ConstDesc* const dp = reinterpret_cast<ConstDesc*>(
-          reinterpret_cast<uintptr_t>(gs.desc + __builtin_amdgcn_readfirstlane(tile)));
-      TileDesc dd;
-      dd.n = dp->n;
-      dd.e0 = dp->e0;
-      dd.e1 = dp->e1;
-      dd.sel = dp->sel;
-#pragma unroll
-      for (int k = 0; k < kDescPieces; ++k) {
-        dd.start[k] = dp->start[k];
-        dd.adj[k] = dp->adj[k];
-      }
-      const int dn = __builtin_amdgcn_readfirstlane(dd.n);
-      // The pieces' base pointers and first tile positions are uniform
-      // (scalar registers); a record picks its piece by compares.  (Read
-      // before the branch: the descriptor's fields arrive in one round trip.)
-      const uint32_t sel = (uint32_t)__builtin_amdgcn_readfirstlane(dd.sel);
-      const Elem* pb[kDescPieces];
-      int st[kDescPieces];
-#pragma unroll
-      for (int k = 0; k < kDescPieces; ++k) {
-        st[k] = __builtin_amdgcn_readfirstlane(dd.start[k]);
-        const uint64_t a = dd.adj[k];
-        const int64_t adj = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(a >> 32)) << 32) |
-                                      (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a));
-        pb[k] = ((sel >> k) & 1u ? gs.A : gs.R) + (tb + adj);
-      }
-#ifdef LSB_GATHER_IDENTITY
-      // Experiment only (wrong in general): a P = 1 loopback gathered pass
-      // reads A in order, so plain loads stand in for the piece lookup.
-      if (LSB_GATHER_IDENTITY) {
-#pragma unroll
-        for (int i = 0; i < IPT; ++i) {
-          const int li = wbase + i * 64;
-          e[i] = li < nvalid ? load_elem_nt(gs.A + tb + li) : Elem{0ull, 0ull};
-        }
-      } else
-#endif
+      const int dn = __builtin_amdgcn_readfirstlane(s_desc.n);
       if (dn != kDescOverflow) {
+        // The pieces' base pointers and first tile positions are uniform
+        // (scalar registers); a record picks its piece by compares.
+        const uint32_t sel = (uint32_t)__builtin_amdgcn_readfirstlane(s_desc.sel);
+        const Elem* pb[kDescPieces];
+        int st[kDescPieces];
+#pragma unroll
+        for (int k = 0; k < kDescPieces; ++k) {
+          st[k] = __builtin_amdgcn_readfirstlane(s_desc.start[k]);
+          const uint64_t a = s_desc.adj[k];
+          const int64_t adj = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(a >> 32)) << 32) |
+                                        (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a));
+          pb[k] = ((sel >> k) & 1u ? gs.A : gs.R) + (tb + adj);
+        }
         // A wave's load i covers tile positions [g0, g0 + 64): when one piece
         // holds them all (every load but the <= 3 that straddle a piece
         // start), its base is picked by scalar compares, not per lane
@@ -1221,7 +1207,7 @@ __device__ __forceinline__ void onesweep_body(
       } else {
         // One record's search at a time (the scheduling barrier keeps the
         // compiler from interleaving 8 searches, which would spill).
-        const int e0 = dd.e0, e1 = dd.e1;
+        const int e0 = s_desc.e0, e1 = s_desc.e1;
 #pragma unroll
         for (int i = 0; i < IPT; ++i) {
           const int li = wbase + i * 64;
@@ -1232,8 +1218,7 @@ __device__ __forceinline__ void onesweep_body(
       }
 #if LSB_GATHER_PF
       // Bring the descriptor of the tile LSB_GATHER_PF ahead in this
-      // sub-array into L2 (this XCD's workgroups take its tiles in order), so
-      // the workgroup that takes it finds it there.
+      // sub-array into L2 (this XCD's workgroups take its tiles in order).
       if (w == 1 && lane == 0) {
         const int pf = tile + LSB_GATHER_PF;
         if (pf < sub_first_tile(x + 1, TT))
@@ -1627,6 +1612,8 @@ __device__ __forceinline__ void onesweep_body(
       }
       if (skewed) write_out(std::true_type{}, h);
       else write_out(std::false_type{}, h);
+      // After wave 0's writes: the grab has returned by then.
+      if (h == HALVES - 1) fetch_desc();
       __syncthreads();
     }
     OS_MARK(4);  // write

@@ -304,6 +304,10 @@ int rec_alloc_group(const lsb_ctx* c, Elem** const* outs, int k, size_t count);
 size_t rec_bytes(size_t count);  // device bytes rec_alloc takes for count records
 void rec_free(void* p);
 bool rec_is_vmm(const void* p);
+// A VMM record buffer that RCCL has seen is being released (an RCCL
+// context's A, B or R): later RCCL contexts of this process take hipMalloc'd
+// record buffers (lsb_alloc.cpp, "RCCL and VMM address reuse").
+void mark_rccl_vmm_released();
 int max_chunks_for_device(int dev);
 // Records A and B are allocated for: the block, or the regional first
 // pass's slots when a P == 1 context's sorts may start with it (blocks of at

@@ -863,3 +863,24 @@ def test_small_vmm_pieces_golden(lsb_built, oracle_mod, digests, monkeypatch, P,
         assert w.verify() == (True, -1)
     with lsb_built.World(1 << 20, ranks=1) as w:  # small buffers: as allocated
         assert w.placement() == {"candidates": 0, "chosen_ms": 0.0, "first_pair_ms": 0.0, "worst_ms": 0.0}
+
+
+def test_rccl_contexts_after_released_vmm_buffers(lsb_built):
+    """Five world-of-one RCCL contexts one after the other in a fresh process
+    (2^28 records, 8-bit digits, every record through ncclAllToAllv in one
+    slice, the placement probe on): each verifies.  With VMM record buffers
+    at addresses of an earlier RCCL context's released ones, RCCL delivered
+    garbage from the third context on (LSB_RCCL_VMM=1 restores that for
+    reproduction); later RCCL contexts now take hipMalloc'd buffers
+    (lsb_alloc.cpp, "RCCL and VMM address reuse")."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, LP_QUICK="1")
+    env.pop("LSB_RCCL_VMM", None)
+    p = subprocess.run([sys.executable, "-u", os.path.join(root, "tools", "r06", "large_call_probe.py"), "28", "8", "1",
+                        "5"], capture_output=True, text=True, timeout=280, cwd=root, env=env)
+    rows = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
+    assert p.returncode == 0 and len(rows) == 5, f"rc={p.returncode}\n{p.stdout[-2000:]}\n{p.stderr[-2000:]}"
+    assert all(r["verified"] for r in rows), rows

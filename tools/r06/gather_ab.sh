@@ -12,9 +12,8 @@ set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R
 O=$R/gpurun_out/${TAG:-r06_gab}; mkdir -p $O
 B=$R/distributed-lsb_amd/build
-declare -A LIB=([base]=$B/liblsb.so [e1]=$B/ab_g_e1/liblsb.so [b4]=$B/ab_g_b4/liblsb.so [b8]=$B/ab_g_b8/liblsb.so
-               [b4l]=$B/ab_g_b4l/liblsb.so [id]=$B/ab_g_id/liblsb.so [ls]=$B/ab_g_ls/liblsb.so [sd]=$B/ab_g_sd/liblsb.so [pf64]=$B/ab_g_pf64/liblsb.so [pf128]=$B/ab_g_pf128/liblsb.so [pf256]=$B/ab_g_pf256/liblsb.so)
-F=${FORMS:-"base e1 b4 b8 b4l"}
+declare -A LIB=([base]=$B/liblsb.so [pre]=$B/ab_pre/liblsb.so [sdesc]=$B/ab_sdesc/liblsb.so [lid]=$B/ab_lid/liblsb.so)
+F=${FORMS:-"pre base lid sdesc"}
 for k in $(seq 1 ${ROUNDS:-3}); do
   list=$F; [ $((k % 2)) = 0 ] && list=$(echo $F | tr ' ' '\n' | tac | tr '\n' ' ')
   for f in $list; do
