@@ -124,7 +124,12 @@ int copy_range(const lsb_ctx*, Rank& dst_rank, Elem* dst, const Rank& src_rank, 
   if (cnt <= 0) return LSB_OK;
   if (!in_buffers(dst_rank, dst, cnt) || !in_buffers(src_rank, src, cnt))
     return fail(LSB_ERR_STATE, "exchange copy", "range outside the record buffers");
-  HIP_TRY(hipMemcpyAsync(dst, src, (size_t)cnt * sizeof(Elem), hipMemcpyDefault, s));
+  if (dst_rank.dev == src_rank.dev) {
+    // One device: a copy kernel (addresses through the page tables only).
+    HIP_TRY(lsb::launch_copy_records(dst, src, cnt, s));
+  } else {
+    HIP_TRY(hipMemcpyAsync(dst, src, (size_t)cnt * sizeof(Elem), hipMemcpyDefault, s));
+  }
   return LSB_OK;
 }
 

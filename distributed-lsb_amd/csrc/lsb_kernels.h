@@ -384,6 +384,8 @@ hipError_t launch_merge_level(const MergeLevel& level, int64_t* path, int grid, 
 
 // O(n) bit-exact stable-sort check of a rank's here-part (see lsb_verify).
 // first_bad must hold UINT64_MAX before the launch; receives min bad global index.
+// cnt records src -> dst on one device (loopback exchange copies).
+hipError_t launch_copy_records(Elem* dst, const Elem* src, int64_t cnt, hipStream_t s);
 hipError_t launch_verify(const Elem* A, int64_t here, int64_t gbase, int64_t n, int64_t per,
                          KeyGen gen, unsigned long long* first_bad, hipStream_t s);
 

@@ -2142,6 +2142,19 @@ __global__ __launch_bounds__(256) void k_gather_desc(GatherSrc g, int64_t m, int
   desc[t] = d;
 }
 
+// ------------------------------------------------------------------ copy
+// A loopback exchange's transfer between two record buffers of one device
+// (copy_range): a plain streaming copy whose addresses go through the GPU's
+// page tables only, not through the runtime's lookup of what a pointer
+// belongs to (hipMemcpyAsync), which has to track VMM ranges as they are
+// mapped, released and mapped again.
+__global__ __launch_bounds__(256) void k_copy_records(Elem* __restrict__ dst, const Elem* __restrict__ src,
+                                                      int64_t cnt) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < cnt; i += stride)
+    store_elem(dst + i, load_elem_nt(src + i));
+}
+
 // ------------------------------------------------------------------ checks
 __global__ __launch_bounds__(256) void k_verify(const Elem* __restrict__ A, int64_t here,
                                                 int64_t gbase, int64_t n, int64_t per, KeyGen gen,
@@ -2543,6 +2556,12 @@ hipError_t launch_gather_desc(const GatherSrc& g, int64_t m, TileDesc* desc, hip
   hipLaunchKernelGGL(k_gather_adj, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, s, g,
                      const_cast<int64_t*>(g.gadj));
   hipLaunchKernelGGL(k_gather_desc, dim3((unsigned)((TT + 255) / 256)), dim3(256), 0, s, g, m, TT, desc);
+  return hipGetLastError();
+}
+
+hipError_t launch_copy_records(Elem* dst, const Elem* src, int64_t cnt, hipStream_t s) {
+  if (cnt <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_copy_records, dim3(grid_for(cnt, 256, 8192)), dim3(256), 0, s, dst, src, cnt);
   return hipGetLastError();
 }
 
