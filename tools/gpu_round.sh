@@ -77,7 +77,7 @@ for s in $RUN; do
     sq)
       SQ_TAG=_$TAG bash tools/sq_counters.sh > $O/sq.log 2>&1 || fail sq $O/sq.log ;;
     stress)
-      timeout -k 10 400 python -u tools/stress_mix.py --seconds ${STRESS_S:-150} --seed ${STRESS_SEED:-7} --max-log2 ${STRESS_LOG2:-27} --trace --stop-on-error \
+      timeout -k 10 400 python -u tools/stress_mix.py --seconds ${STRESS_S:-150} --seed ${STRESS_SEED:-7} --max-log2 ${STRESS_LOG2:-27} --rccl-share ${STRESS_RCCL:-0} --trace --stop-on-error \
         > $O/stress_mix.log 2>&1 || fail stress $O/stress_mix.log
       tail -1 $O/stress_mix.log
       grep -q "done: 0 of" $O/stress_mix.log || fail stress $O/stress_mix.log ;;

@@ -18,8 +18,11 @@ overflow one and start over); each line names how the sort began.  One
 draw in three sets LSB_PLACEMENT_CANDIDATES=4 (the placement probe for the
 P = 1 buffers of >= 1 GiB, built from the drawn pieces), the others 0; and
 three draws in five send 16-bit exchanges in 2, 4 or 8 chunks
-(LSB_OPT_EXCHANGE_CHUNKS, blocks of >= 2^16 records).  Runs until
---seconds have passed; one line per iteration.
+(LSB_OPT_EXCHANGE_CHUNKS, blocks of >= 2^16 records).  --rccl-share runs a
+share of the iterations as world-of-one RCCL contexts instead (every record
+through ncclAllToAllv; the context kind where RCCL over reused VMM addresses
+went wrong).  Runs until --seconds have passed; one line per
+iteration.
 
     python tools/stress_mix.py --seconds 240 --seed 1
 """
@@ -139,22 +142,36 @@ def main():
                     help="an earlier round's draws (as tools/stress_replay.py): r05v12 without the probe and "
                          "chunk draws, r05 without the chunk draw")
     ap.add_argument("--iters", type=int, default=0, help="stop after this many sorts (0: --seconds only)")
+    ap.add_argument("--rccl-share", type=float, default=0.0,
+                    help="share of iterations run as a world-of-one RCCL context (P = 1, exchange forced, every "
+                         "record through ncclAllToAllv), drawn from a second generator so the other draws stay "
+                         "those of --seed")
     a = ap.parse_args()
     rng = random.Random(a.seed)
+    rng_rccl = random.Random(a.seed ^ 0x5EED5EED)
     t_end = time.time() + a.seconds
     it = bad = 0
     while time.time() < t_end and (a.iters <= 0 or it < a.iters):
         cfg = draw(rng, a.max_log2, a.draws, a.host_share, a.hybrid)
         set_env(cfg)
+        rccl = rng_rccl.random() < a.rccl_share
+        if rccl:
+            cfg["P"] = 1
         n, P, bits, dist = cfg["n"], cfg["P"], cfg["bits"], cfg["dist"]
         desc = (f"iter {it}: n={n} P={P} bits={bits} dist={dist} split={cfg['split']} hybrid={cfg['hybrid']} "
                 f"gather={cfg['gather']} vmm={cfg['vmm']} region_min={cfg['region_min']} probe={cfg['probe']} "
-                f"chunks={cfg['chunks']}")
+                f"chunks={cfg['chunks']}" + (" rccl=1" if rccl else ""))
         t0 = time.time()
         if a.trace:  # the configuration before the sort: a fault kills the process mid-sort
             print(f"begin {desc}", flush=True)
         try:
-            with lsbsort.World(n, ranks=P, radix_bits=bits) as w:
+            if rccl:
+                w = lsbsort.World.rank(n, 1, 0, 0, lsbsort.get_unique_id(), radix_bits=bits)
+                w.set_option(lsbsort.OPT_FORCE_EXCHANGE, 1)
+                w.set_option(lsbsort.OPT_EXCHANGE_SELF, 1)
+            else:
+                w = lsbsort.World(n, ranks=P, radix_bits=bits)
+            with w:
                 set_options(w, cfg)
                 if cfg["host"]:
                     arr = host_keys(rng, cfg)
