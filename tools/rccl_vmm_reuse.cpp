@@ -1,0 +1,168 @@
+// Pure-RCCL check of VMM buffers at reused addresses (no liblsb): the round-6
+// wrong answer of test_world_of_one_large_calls[28-8-1] came from world-of-one
+// RCCL contexts whose record buffers (HIP VMM: reserved address range, 1 GiB
+// physical pieces) were mapped at addresses an earlier context's released
+// buffers had used (profiles/r06/large_call/).  This program
+// does what those contexts did, with RCCL alone: per iteration a fresh
+// world-of-one communicator, a send and a receive buffer of S GiB built from
+// 1 GiB pieces, D decoy buffers allocated and released first (the placement
+// probe's losing candidates), then R rounds of ncclAllToAllv of the whole
+// buffer to the rank itself, cut into 1 GiB calls (coll_alltoallv_u64), each
+// checked on the device; then everything released.  One JSON line per
+// iteration with the buffers' addresses and the wrong u64 count.
+//
+//   tools/rccl_vmm_reuse ITERS SIZE_GIB DECOYS ROUNDS [malloc]
+//
+// Build: hipcc --offload-arch=gfx950 -O2 tools/rccl_vmm_reuse.cpp -lrccl (tools/rccl_vmm_reuse.sh).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+namespace {
+
+#define CK(x)                                                                  \
+  do {                                                                         \
+    hipError_t e_ = (x);                                                       \
+    if (e_ != hipSuccess) {                                                    \
+      fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));                  \
+      exit(2);                                                                 \
+    }                                                                          \
+  } while (0)
+#define CN(x)                                                                  \
+  do {                                                                         \
+    ncclResult_t r_ = (x);                                                     \
+    if (r_ != ncclSuccess) {                                                   \
+      fprintf(stderr, "%s: %s\n", #x, ncclGetErrorString(r_));                 \
+      exit(3);                                                                 \
+    }                                                                          \
+  } while (0)
+
+constexpr size_t kPiece = size_t(1) << 30;
+
+__host__ __device__ inline uint64_t value_of(uint64_t it, uint64_t round, uint64_t i) {
+  uint64_t x = (it << 56) ^ (round << 48) ^ i;
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdULL;
+  x ^= x >> 33;
+  return x;
+}
+
+__global__ void k_fill(uint64_t* p, uint64_t n, uint64_t it, uint64_t round) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    p[i] = value_of(it, round, i);
+}
+
+__global__ void k_check(const uint64_t* p, uint64_t n, uint64_t it, uint64_t round, unsigned long long* bad) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    if (p[i] != value_of(it, round, i)) atomicAdd(bad, 1ull);
+}
+
+struct Buf {
+  void* base = nullptr;
+  size_t bytes = 0;
+  std::vector<hipMemGenericAllocationHandle_t> pieces;
+  bool vmm = true;
+};
+
+Buf alloc_buf(size_t bytes, bool vmm) {
+  Buf b;
+  b.bytes = bytes;
+  b.vmm = vmm;
+  if (!vmm) {
+    CK(hipMalloc(&b.base, bytes));
+    return b;
+  }
+  hipMemAllocationProp prop = {};
+  prop.type = hipMemAllocationTypePinned;
+  prop.location.type = hipMemLocationTypeDevice;
+  prop.location.id = 0;
+  CK(hipMemAddressReserve(&b.base, bytes, kPiece, nullptr, 0));
+  for (size_t off = 0; off < bytes; off += kPiece) {
+    hipMemGenericAllocationHandle_t h;
+    CK(hipMemCreate(&h, kPiece, &prop, 0));
+    CK(hipMemMap(static_cast<char*>(b.base) + off, kPiece, 0, h, 0));
+    b.pieces.push_back(h);
+  }
+  hipMemAccessDesc a = {};
+  a.location.type = hipMemLocationTypeDevice;
+  a.location.id = 0;
+  a.flags = hipMemAccessFlagsProtReadWrite;
+  CK(hipMemSetAccess(b.base, bytes, &a, 1));
+  return b;
+}
+
+void free_buf(Buf& b) {
+  CK(hipDeviceSynchronize());
+  if (!b.vmm) {
+    CK(hipFree(b.base));
+  } else {
+    for (size_t k = 0; k < b.pieces.size(); ++k) CK(hipMemUnmap(static_cast<char*>(b.base) + k * kPiece, kPiece));
+    for (auto h : b.pieces) CK(hipMemRelease(h));
+    CK(hipMemAddressFree(b.base, b.bytes));
+  }
+  b = Buf();
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  if (argc < 5) {
+    fprintf(stderr, "usage: %s ITERS SIZE_GIB DECOYS ROUNDS [malloc]\n", argv[0]);
+    return 1;
+  }
+  const int iters = atoi(argv[1]), decoys = atoi(argv[3]), rounds = atoi(argv[4]);
+  const size_t bytes = (size_t)atoi(argv[2]) * kPiece;
+  const bool vmm = !(argc > 5 && !strcmp(argv[5], "malloc"));
+  const uint64_t n = bytes / 8, call = kPiece / 8;  // u64 in all, per call
+  CK(hipSetDevice(0));
+  int version = 0;
+  (void)ncclGetVersion(&version);
+  printf("{\"rccl_version\": %d, \"gib\": %zu, \"decoys\": %d, \"rounds\": %d, \"vmm\": %s}\n", version,
+         bytes >> 30, decoys, rounds, vmm ? "true" : "false");
+  fflush(stdout);
+  unsigned long long* bad = nullptr;
+  CK(hipMalloc(&bad, sizeof(unsigned long long)));
+  int worst = 0;
+  for (int it = 0; it < iters; ++it) {
+    ncclUniqueId id;
+    CN(ncclGetUniqueId(&id));
+    ncclComm_t comm;
+    CN(ncclCommInitRank(&comm, 1, id, 0));
+    hipStream_t s;
+    CK(hipStreamCreate(&s));
+    std::vector<Buf> decoy;
+    for (int d = 0; d < decoys; ++d) decoy.push_back(alloc_buf(bytes, vmm));
+    Buf snd = alloc_buf(bytes, vmm), rcv = alloc_buf(bytes, vmm);
+    for (Buf& d : decoy) free_buf(d);
+    unsigned long long wrong = 0;
+    for (int r = 0; r < rounds; ++r) {
+      k_fill<<<4096, 256, 0, s>>>(static_cast<uint64_t*>(snd.base), n, it, r);
+      CK(hipMemsetAsync(rcv.base, 0, bytes, s));
+      for (uint64_t off = 0; off < n; off += call) {  // calls of at most 1 GiB, as the runtime cuts them
+        size_t cnt = n - off < call ? n - off : call, zero = 0;
+        CN(ncclAllToAllv(static_cast<uint64_t*>(snd.base) + off, &cnt, &zero,
+                         static_cast<uint64_t*>(rcv.base) + off, &cnt, &zero, ncclUint64, comm, s));
+      }
+      CK(hipMemsetAsync(bad, 0, sizeof(unsigned long long), s));
+      k_check<<<4096, 256, 0, s>>>(static_cast<const uint64_t*>(rcv.base), n, it, r, bad);
+      unsigned long long h = 0;
+      CK(hipMemcpyAsync(&h, bad, sizeof h, hipMemcpyDeviceToHost, s));
+      CK(hipStreamSynchronize(s));
+      wrong += h;
+    }
+    printf("{\"iter\": %d, \"send\": \"%p\", \"recv\": \"%p\", \"wrong_u64\": %llu}\n", it, snd.base, rcv.base, wrong);
+    fflush(stdout);
+    if (wrong) worst = 1;
+    free_buf(snd);
+    free_buf(rcv);
+    CK(hipStreamDestroy(s));
+    CN(ncclCommDestroy(comm));
+  }
+  CK(hipFree(bad));
+  return worst;
+}
