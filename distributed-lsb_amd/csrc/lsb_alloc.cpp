@@ -53,15 +53,17 @@ void vmm_release(VmmBuffer& b, size_t piece) {
   b = VmmBuffer();
 }
 
-// RCCL and VMM address reuse.  RCCL 2.27.7 over VMM record buffers mapped at
-// addresses that an earlier RCCL context's (released) VMM buffers had used
-// delivered garbage: a world-of-one context sorting 2^28 records with 8-bit
+// RCCL and VMM address reuse.  RCCL contexts (RCCL 2.27.7) over VMM record
+// buffers mapped at addresses that an earlier RCCL context's (released) VMM
+// buffers had used delivered garbage: a world-of-one context sorting 2^28 records with 8-bit
 // digits through ncclAllToAllv failed lsb_verify from its process's third
 // such context on (zeros at the head, records lost; 3 of 5 and 3 of 6 sorts),
 // never with hipMalloc'd buffers (5 of 5), nor while released address ranges
 // stayed reserved (6 of 6, but then their memory is not given back: 288 ->
 // 147 GiB free after 4 contexts); the reservation's address hint is not
-// honoured, so the runtime hands the same ranges out again.
+// honoured, so the runtime hands the same ranges out again.  RCCL alone over
+// VMM buffers at reused addresses (tools/rccl_vmm_reuse.cpp) stayed right, so
+// which layer fails is open; the rule below avoids it either way.
 // profiles/r06/large_call/, tests/test_gpu_sort.py
 // test_world_of_one_large_calls.  So once a VMM buffer of an
 // RCCL context has been released in this process, later RCCL contexts take
