@@ -11,7 +11,8 @@
 // checked on the device; then everything released.  One JSON line per
 // iteration with the buffers' addresses and the wrong u64 count.
 //
-//   tools/rccl_vmm_reuse ITERS SIZE_GIB DECOYS ROUNDS [malloc]
+//   tools/rccl_vmm_reuse ITERS SIZE_GIB DECOYS ROUNDS [malloc|swap]
+//   (swap: odd iterations back the reused ranges with other physical pieces)
 //
 // Build: hipcc --offload-arch=gfx950 -O2 tools/rccl_vmm_reuse.cpp -lrccl (tools/rccl_vmm_reuse.sh).
 #include <hip/hip_runtime.h>
@@ -69,7 +70,7 @@ struct Buf {
   bool vmm = true;
 };
 
-Buf alloc_buf(size_t bytes, bool vmm) {
+Buf reserve_buf(size_t bytes, bool vmm) {
   Buf b;
   b.bytes = bytes;
   b.vmm = vmm;
@@ -77,14 +78,24 @@ Buf alloc_buf(size_t bytes, bool vmm) {
     CK(hipMalloc(&b.base, bytes));
     return b;
   }
+  CK(hipMemAddressReserve(&b.base, bytes, kPiece, nullptr, 0));
+  return b;
+}
+
+hipMemGenericAllocationHandle_t make_piece() {
   hipMemAllocationProp prop = {};
   prop.type = hipMemAllocationTypePinned;
   prop.location.type = hipMemLocationTypeDevice;
   prop.location.id = 0;
-  CK(hipMemAddressReserve(&b.base, bytes, kPiece, nullptr, 0));
-  for (size_t off = 0; off < bytes; off += kPiece) {
-    hipMemGenericAllocationHandle_t h;
-    CK(hipMemCreate(&h, kPiece, &prop, 0));
+  hipMemGenericAllocationHandle_t h;
+  CK(hipMemCreate(&h, kPiece, &prop, 0));
+  return h;
+}
+
+void back_buf(Buf& b) {  // physical pieces for a reserved range, mapped in order
+  if (!b.vmm) return;
+  for (size_t off = 0; off < b.bytes; off += kPiece) {
+    hipMemGenericAllocationHandle_t h = make_piece();
     CK(hipMemMap(static_cast<char*>(b.base) + off, kPiece, 0, h, 0));
     b.pieces.push_back(h);
   }
@@ -92,7 +103,12 @@ Buf alloc_buf(size_t bytes, bool vmm) {
   a.location.type = hipMemLocationTypeDevice;
   a.location.id = 0;
   a.flags = hipMemAccessFlagsProtReadWrite;
-  CK(hipMemSetAccess(b.base, bytes, &a, 1));
+  CK(hipMemSetAccess(b.base, b.bytes, &a, 1));
+}
+
+Buf alloc_buf(size_t bytes, bool vmm) {
+  Buf b = reserve_buf(bytes, vmm);
+  back_buf(b);
   return b;
 }
 
@@ -112,18 +128,19 @@ void free_buf(Buf& b) {
 
 int main(int argc, char** argv) {
   if (argc < 5) {
-    fprintf(stderr, "usage: %s ITERS SIZE_GIB DECOYS ROUNDS [malloc]\n", argv[0]);
+    fprintf(stderr, "usage: %s ITERS SIZE_GIB DECOYS ROUNDS [malloc|swap]\n", argv[0]);
     return 1;
   }
   const int iters = atoi(argv[1]), decoys = atoi(argv[3]), rounds = atoi(argv[4]);
   const size_t bytes = (size_t)atoi(argv[2]) * kPiece;
   const bool vmm = !(argc > 5 && !strcmp(argv[5], "malloc"));
+  const bool swap = argc > 5 && !strcmp(argv[5], "swap");
   const uint64_t n = bytes / 8, call = kPiece / 8;  // u64 in all, per call
   CK(hipSetDevice(0));
   int version = 0;
   (void)ncclGetVersion(&version);
-  printf("{\"rccl_version\": %d, \"gib\": %zu, \"decoys\": %d, \"rounds\": %d, \"vmm\": %s}\n", version,
-         bytes >> 30, decoys, rounds, vmm ? "true" : "false");
+  printf("{\"rccl_version\": %d, \"gib\": %zu, \"decoys\": %d, \"rounds\": %d, \"vmm\": %s, \"swap\": %s}\n", version,
+         bytes >> 30, decoys, rounds, vmm ? "true" : "false", swap ? "true" : "false");
   fflush(stdout);
   unsigned long long* bad = nullptr;
   CK(hipMalloc(&bad, sizeof(unsigned long long)));
@@ -137,7 +154,19 @@ int main(int argc, char** argv) {
     CK(hipStreamCreate(&s));
     std::vector<Buf> decoy;
     for (int d = 0; d < decoys; ++d) decoy.push_back(alloc_buf(bytes, vmm));
-    Buf snd = alloc_buf(bytes, vmm), rcv = alloc_buf(bytes, vmm);
+    // swap: on odd iterations the ranges are backed in the other order, after
+    // a held spacer piece, so a reused address range gets other physical
+    // memory than it had (as when the placement probe picks another candidate).
+    Buf snd = reserve_buf(bytes, vmm), rcv = reserve_buf(bytes, vmm);
+    std::vector<hipMemGenericAllocationHandle_t> spacer;
+    if (swap && vmm && (it & 1)) {
+      spacer.push_back(make_piece());
+      back_buf(rcv);
+      back_buf(snd);
+    } else {
+      back_buf(snd);
+      back_buf(rcv);
+    }
     for (Buf& d : decoy) free_buf(d);
     unsigned long long wrong = 0;
     for (int r = 0; r < rounds; ++r) {
@@ -160,6 +189,7 @@ int main(int argc, char** argv) {
     if (wrong) worst = 1;
     free_buf(snd);
     free_buf(rcv);
+    for (auto h : spacer) CK(hipMemRelease(h));
     CK(hipStreamDestroy(s));
     CN(ncclCommDestroy(comm));
   }
