@@ -61,9 +61,13 @@ void vmm_release(VmmBuffer& b, size_t piece) {
 // never with hipMalloc'd buffers (5 of 5), nor while released address ranges
 // stayed reserved (6 of 6, but then their memory is not given back: 288 ->
 // 147 GiB free after 4 contexts); the reservation's address hint is not
-// honoured, so the runtime hands the same ranges out again.  RCCL alone over
-// VMM buffers at reused addresses (tools/rccl_vmm_reuse.cpp) stayed right, so
-// which layer fails is open; the rule below avoids it either way.
+// honoured, so the runtime hands the same ranges out again.  It needs records
+// through RCCL (loopback contexts with the same buffers, and RCCL contexts
+// sending no record through RCCL, stay right), is no stream race (it stays
+// with the device drained around every call, LSB_RCCL_SYNC=1) and no
+// leftover-data artefact (other input per context: same picture).  RCCL
+// alone over VMM buffers at reused addresses (tools/rccl_vmm_reuse.cpp)
+// stayed right, so which layer fails is open; the rule below avoids it.
 // profiles/r06/large_call/, tests/test_gpu_sort.py
 // test_world_of_one_large_calls.  So once a VMM buffer of an
 // RCCL context has been released in this process, later RCCL contexts take

@@ -308,6 +308,10 @@ int coll_alltoallv_u64(lsb_ctx* c, Rank& r, const uint64_t* send, const size_t* 
   }
   if (c->cur_pass >= 0 && c->cur_pass < LSB_MAX_PASSES) c->pass_xbytes[c->cur_pass] += call_bytes;
   if (c->mode == Mode::kRccl) {
+    // LSB_RCCL_SYNC=1 (diagnostic): the device drains before and after every
+    // call, so no work of any stream overlaps it.
+    static const bool dsync = [] { const char* e = getenv("LSB_RCCL_SYNC"); return e && atoi(e); }();
+    if (dsync) HIP_TRY(hipDeviceSynchronize());
     if (!c->p2p) {
       RCCL_TRY(ncclAllToAllv(send, sc, sd, recv, rc, rd, ncclUint64, c->comm, st));
     } else {  // the same exchange as explicit grouped point-to-point calls
@@ -318,6 +322,7 @@ int coll_alltoallv_u64(lsb_ctx* c, Rank& r, const uint64_t* send, const size_t* 
       }
       RCCL_TRY(ncclGroupEnd());
     }
+    if (dsync) HIP_TRY(hipDeviceSynchronize());
     return LSB_OK;
   }
   size_t send_end = 0, recv_end = 0;

@@ -869,10 +869,10 @@ def test_rccl_contexts_after_released_vmm_buffers(lsb_built):
     """Five world-of-one RCCL contexts one after the other in a fresh process
     (2^28 records, 8-bit digits, every record through ncclAllToAllv in one
     slice, the placement probe on): each verifies.  With VMM record buffers
-    at addresses of an earlier RCCL context's released ones, RCCL delivered
-    garbage from the third context on (LSB_RCCL_VMM=1 restores that for
-    reproduction); later RCCL contexts now take hipMalloc'd buffers
-    (lsb_alloc.cpp, "RCCL and VMM address reuse")."""
+    at addresses of an earlier RCCL context's released ones, records through
+    RCCL came back as garbage from the third context on (LSB_RCCL_VMM=1
+    restores that for reproduction); later RCCL contexts now take hipMalloc'd
+    buffers (lsb_alloc.cpp, "RCCL and VMM address reuse")."""
     import json
     import subprocess
     import sys
@@ -883,4 +883,25 @@ def test_rccl_contexts_after_released_vmm_buffers(lsb_built):
                         "5"], capture_output=True, text=True, timeout=280, cwd=root, env=env)
     rows = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
     assert p.returncode == 0 and len(rows) == 5, f"rc={p.returncode}\n{p.stdout[-2000:]}\n{p.stderr[-2000:]}"
+    assert all(r["verified"] for r in rows), rows
+
+
+def test_rccl_contexts_after_released_vmm_buffers_other_input(lsb_built):
+    """As above with other random input in every context (LP_SEED=1: checked
+    on the host -- keys with their values, values a permutation, stable
+    order), so no context can pass on an earlier context's leftovers in a
+    buffer: four contexts, the third and fourth being the ones that failed
+    with VMM buffers at reused addresses (DESIGN.md §0,
+    profiles/r06/large_call/r06_g28/)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, LP_QUICK="1", LP_SEED="1")
+    env.pop("LSB_RCCL_VMM", None)
+    p = subprocess.run([sys.executable, "-u", os.path.join(root, "tools", "r06", "large_call_probe.py"), "28", "8", "1",
+                        "4"], capture_output=True, text=True, timeout=280, cwd=root, env=env)
+    rows = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
+    assert p.returncode == 0 and len(rows) == 4, f"rc={p.returncode}\n{p.stdout[-2000:]}\n{p.stderr[-2000:]}"
+    assert all(r["seeded"] for r in rows), rows
     assert all(r["verified"] for r in rows), rows

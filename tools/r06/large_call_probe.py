@@ -8,7 +8,9 @@ blocks, the size of one cut RCCL call), and whether the output is still a
 permutation of the input (records misplaced) or not (records lost).
 
     python tools/r06/large_call_probe.py [lg=28] [bits=8] [slices=1] [reps=3]
-    (env: LSB_RCCL_CALL_U64, OPT via LP_GATHER=0/1)
+    (env: LSB_RCCL_CALL_U64, OPTs via LP_GATHER=0/1, LP_P2P=0/1;
+     LP_LOOPBACK=1: a loopback context; LP_NOFORCE=1: no forced exchange;
+     LP_SEED=1: other random input per repetition)
 """
 import json
 import os
@@ -22,21 +24,48 @@ import lsbsort  # noqa: E402
 lg, bits, slices, reps = (int(x) for x in (sys.argv[1:] + ["28", "8", "1", "3"][len(sys.argv) - 1:])[:4])
 n = 1 << lg
 for rep in range(reps):
-    w = lsbsort.World.rank(n, 1, 0, 0, lsbsort.get_unique_id(), radix_bits=bits)
+    if os.environ.get("LP_LOOPBACK"):  # a loopback context: the same sort, no RCCL
+        w = lsbsort.World(n, ranks=1, radix_bits=bits)
+    else:
+        w = lsbsort.World.rank(n, 1, 0, 0, lsbsort.get_unique_id(), radix_bits=bits)
     try:
-        w.set_option(lsbsort.OPT_FORCE_EXCHANGE, 1)
+        w.set_option(lsbsort.OPT_FORCE_EXCHANGE, 0 if os.environ.get("LP_NOFORCE") else 1)
         w.set_option(lsbsort.OPT_EXCHANGE_SELF, 1)
         if slices:
             w.set_option(lsbsort.OPT_EXCHANGE_SLICES, slices)
+        if os.environ.get("LP_P2P"):
+            w.set_option(lsbsort.OPT_EXCHANGE_P2P, int(os.environ["LP_P2P"]))
         if os.environ.get("LP_GATHER"):
             w.set_option(lsbsort.OPT_EXCHANGE_GATHER, int(os.environ["LP_GATHER"]))
-        w.generate()
+        if os.environ.get("LP_SEED"):  # other input per repetition (generate() is pcg64(rank) every time)
+            rng = np.random.default_rng(1000 + rep)
+            arr = np.empty(n, dtype=lsbsort.ELEM_DTYPE)
+            arr["key"] = rng.integers(0, np.iinfo(np.uint64).max, size=n, dtype=np.uint64, endpoint=True)
+            arr["val"] = np.arange(n, dtype=np.uint64)
+            w.copy_in(0, arr)
+            keys_in = arr["key"].copy()
+            del arr
+        else:
+            w.generate()
         inp = w.copy_out(0)
         w.my_sort()
         w.sync()
-        ok, first = w.verify()
+        if os.environ.get("LP_SEED"):  # lsb_verify checks against generate()'s input: check on the host
+            out = w.copy_out(0)
+            k, v = out["key"], out["val"]
+            ok = bool((v < n).all()) and bool(np.bincount(v.astype(np.int64), minlength=n).max() == 1)
+            ok = ok and bool(np.array_equal(k, keys_in[v.astype(np.int64)]))  # every key with its value
+            step = (k[1:] > k[:-1]) | ((k[1:] == k[:-1]) & (v[1:] > v[:-1]))  # stable order
+            bad = np.nonzero(~step)[0]
+            first = int(bad[0]) if bad.size else -1
+            ok = ok and first < 0
+            del out, k, v, step
+        else:
+            ok, first = w.verify()
         row = {"rep": rep, "lg": lg, "bits": bits, "slices": slices, "call_u64": os.environ.get("LSB_RCCL_CALL_U64"),
-               "gather": os.environ.get("LP_GATHER"), "verified": ok, "first_bad": first,
+               "gather": os.environ.get("LP_GATHER"), "p2p": os.environ.get("LP_P2P"), "loopback": bool(os.environ.get("LP_LOOPBACK")),
+               "noforce": bool(os.environ.get("LP_NOFORCE")), "seeded": bool(os.environ.get("LP_SEED")),
+               "rccl_vmm": os.environ.get("LSB_RCCL_VMM"), "rccl_sync": os.environ.get("LSB_RCCL_SYNC"), "verified": ok, "first_bad": first,
                "exchanges": w.exchange_stats()["exchanges"], "calls": w.exchange_stats()["calls"]}
         print(json.dumps(row), flush=True)
         if not ok and not os.environ.get("LP_QUICK"):
