@@ -65,9 +65,12 @@ void vmm_release(VmmBuffer& b, size_t piece) {
 // through RCCL (loopback contexts with the same buffers, and RCCL contexts
 // sending no record through RCCL, stay right), is no stream race (it stays
 // with the device drained around every call, LSB_RCCL_SYNC=1) and no
-// leftover-data artefact (other input per context: same picture).  RCCL
-// alone over VMM buffers at reused addresses (tools/rccl_vmm_reuse.cpp)
-// stayed right, so which layer fails is open; the rule below avoids it.
+// leftover-data artefact (other input per context: same picture).  It is
+// reproduced without liblsb and without RCCL (tools/rccl_vmm_reuse.cpp
+// late ... kernel): ranges written by the GPU, released, and a range then
+// mapped onto their addresses read back wrong through a plain copy kernel
+// (never-written ranges and hipMalloc stay right), so the fault is in
+// HIP/ROCm's VMM, and the rule below is a workaround for where we met it.
 // profiles/r06/large_call/, tests/test_gpu_sort.py
 // test_world_of_one_large_calls.  So once a VMM buffer of an
 // RCCL context has been released in this process, later RCCL contexts take

@@ -350,8 +350,8 @@ int  lsb_get_pass_exchange(lsb_ctx_t* ctx, int pass, int64_t* bytes, double* wir
  * at least 1 GiB are built from 1 GiB physical pieces (HIP virtual memory;
  * LSB_RECORD_ALLOC=malloc: hipMalloc) -- except in an RCCL context created
  * after an earlier RCCL context of the process released such buffers: such
- * contexts returned wrong data over pieces mapped at reused addresses (RCCL
- * alone did not reproduce it), so those take
+ * contexts returned wrong data over pieces mapped at reused addresses (a
+ * HIP VMM fault, reproduced with a copy kernel alone), so those take
  * hipMalloc'd buffers (LSB_RCCL_VMM=1: pieces regardless).
  * Such a buffer can still be a slow
  * pass destination as a whole, so a rank whose buffers hold

@@ -872,7 +872,8 @@ def test_rccl_contexts_after_released_vmm_buffers(lsb_built):
     at addresses of an earlier RCCL context's released ones, records through
     RCCL came back as garbage from the third context on (LSB_RCCL_VMM=1
     restores that for reproduction); later RCCL contexts now take hipMalloc'd
-    buffers (lsb_alloc.cpp, "RCCL and VMM address reuse")."""
+    buffers (lsb_alloc.cpp, "RCCL and VMM address reuse"; the fault is in
+    HIP's VMM, reproduced without RCCL by tools/rccl_vmm_reuse.cpp)."""
     import json
     import subprocess
     import sys

@@ -11,8 +11,9 @@
 // checked on the device; then everything released.  One JSON line per
 // iteration with the buffers' addresses and the wrong u64 count.
 //
-//   tools/rccl_vmm_reuse ITERS SIZE_GIB DECOYS ROUNDS [malloc|swap]
-//   (swap: odd iterations back the reused ranges with other physical pieces)
+//   tools/rccl_vmm_reuse ITERS SIZE_GIB DECOYS ROUNDS [malloc|swap|late|vmm] [rccl|memcpy|kernel] [nofill]
+//   (swap: odd iterations back the reused ranges with other physical pieces;
+//    late: decoys written, released, then the receive buffer allocated)
 //
 // Build: hipcc --offload-arch=gfx950 -O2 tools/rccl_vmm_reuse.cpp -lrccl (tools/rccl_vmm_reuse.sh).
 #include <hip/hip_runtime.h>
@@ -61,6 +62,11 @@ __global__ void k_fill(uint64_t* p, uint64_t n, uint64_t it, uint64_t round) {
 __global__ void k_check(const uint64_t* p, uint64_t n, uint64_t it, uint64_t round, unsigned long long* bad) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     if (p[i] != value_of(it, round, i)) atomicAdd(bad, 1ull);
+}
+
+__global__ void k_copy(uint64_t* dst, const uint64_t* src, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    dst[i] = src[i];
 }
 
 struct Buf {
@@ -128,19 +134,23 @@ void free_buf(Buf& b) {
 
 int main(int argc, char** argv) {
   if (argc < 5) {
-    fprintf(stderr, "usage: %s ITERS SIZE_GIB DECOYS ROUNDS [malloc|swap]\n", argv[0]);
+    fprintf(stderr, "usage: %s ITERS SIZE_GIB DECOYS ROUNDS [malloc|swap|late|vmm] [rccl|memcpy|kernel] [nofill]\n", argv[0]);
     return 1;
   }
   const int iters = atoi(argv[1]), decoys = atoi(argv[3]), rounds = atoi(argv[4]);
   const size_t bytes = (size_t)atoi(argv[2]) * kPiece;
   const bool vmm = !(argc > 5 && !strcmp(argv[5], "malloc"));
   const bool swap = argc > 5 && !strcmp(argv[5], "swap");
+  const bool late = argc > 5 && !strcmp(argv[5], "late");
+  // transport (argv[6]): rccl (default) | memcpy (hipMemcpyAsync) | kernel (a copy kernel)
+  const bool nofill = argc > 7 && !strcmp(argv[7], "nofill");  // late: decoys never written
+  const int transport = argc > 6 ? (!strcmp(argv[6], "memcpy") ? 1 : !strcmp(argv[6], "kernel") ? 2 : 0) : 0;
   const uint64_t n = bytes / 8, call = kPiece / 8;  // u64 in all, per call
   CK(hipSetDevice(0));
   int version = 0;
   (void)ncclGetVersion(&version);
-  printf("{\"rccl_version\": %d, \"gib\": %zu, \"decoys\": %d, \"rounds\": %d, \"vmm\": %s, \"swap\": %s}\n", version,
-         bytes >> 30, decoys, rounds, vmm ? "true" : "false", swap ? "true" : "false");
+  printf("{\"rccl_version\": %d, \"gib\": %zu, \"decoys\": %d, \"rounds\": %d, \"vmm\": %s, \"swap\": %s, \"late\": %s, \"transport\": %d, \"nofill\": %s}\n", version,
+         bytes >> 30, decoys, rounds, vmm ? "true" : "false", swap ? "true" : "false", late ? "true" : "false", transport, nofill ? "true" : "false");
   fflush(stdout);
   unsigned long long* bad = nullptr;
   CK(hipMalloc(&bad, sizeof(unsigned long long)));
@@ -157,13 +167,28 @@ int main(int argc, char** argv) {
     // swap: on odd iterations the ranges are backed in the other order, after
     // a held spacer piece, so a reused address range gets other physical
     // memory than it had (as when the placement probe picks another candidate).
-    Buf snd = reserve_buf(bytes, vmm), rcv = reserve_buf(bytes, vmm);
+    Buf snd, rcv;
     std::vector<hipMemGenericAllocationHandle_t> spacer;
-    if (swap && vmm && (it & 1)) {
+    if (late) {
+      // liblsb's order: the probe's candidates (the send buffer among them)
+      // are written by timed passes, the losers released, and the receive
+      // buffer is allocated at the first exchange, onto a released range.
+      snd = alloc_buf(bytes, vmm);
+      if (!nofill)
+        for (Buf& d : decoy) k_fill<<<4096, 256, 0, s>>>(static_cast<uint64_t*>(d.base), n, it, 99);
+      CK(hipStreamSynchronize(s));
+      for (Buf& d : decoy) free_buf(d);
+      decoy.clear();
+      rcv = alloc_buf(bytes, vmm);
+    } else if (swap && vmm && (it & 1)) {
+      snd = reserve_buf(bytes, vmm);
+      rcv = reserve_buf(bytes, vmm);
       spacer.push_back(make_piece());
       back_buf(rcv);
       back_buf(snd);
     } else {
+      snd = reserve_buf(bytes, vmm);
+      rcv = reserve_buf(bytes, vmm);
       back_buf(snd);
       back_buf(rcv);
     }
@@ -174,8 +199,15 @@ int main(int argc, char** argv) {
       CK(hipMemsetAsync(rcv.base, 0, bytes, s));
       for (uint64_t off = 0; off < n; off += call) {  // calls of at most 1 GiB, as the runtime cuts them
         size_t cnt = n - off < call ? n - off : call, zero = 0;
-        CN(ncclAllToAllv(static_cast<uint64_t*>(snd.base) + off, &cnt, &zero,
-                         static_cast<uint64_t*>(rcv.base) + off, &cnt, &zero, ncclUint64, comm, s));
+        uint64_t* src = static_cast<uint64_t*>(snd.base) + off;
+        uint64_t* dst = static_cast<uint64_t*>(rcv.base) + off;
+        if (transport == 1) {
+          CK(hipMemcpyAsync(dst, src, cnt * 8, hipMemcpyDeviceToDevice, s));
+        } else if (transport == 2) {
+          k_copy<<<4096, 256, 0, s>>>(dst, src, cnt);
+        } else {
+          CN(ncclAllToAllv(src, &cnt, &zero, dst, &cnt, &zero, ncclUint64, comm, s));
+        }
       }
       CK(hipMemsetAsync(bad, 0, sizeof(unsigned long long), s));
       k_check<<<4096, 256, 0, s>>>(static_cast<const uint64_t*>(rcv.base), n, it, r, bad);

@@ -5,7 +5,11 @@
 # run): with 2 decoy buffers released first (as the placement probe's
 # losers), without decoys, and with hipMalloc'd buffers.  MODE=swap: odd
 # iterations back the reused ranges with other physical pieces, with 0 and 2
-# decoys.  Stops at the first run that ends other than 0 (right) or 1 (wrong).
+# decoys.  MODE=late: the decoys written and released, then the receive
+# buffer allocated (liblsb's order), with 2 and 3 decoys.  MODE=transport:
+# late with hipMemcpyAsync, a copy kernel, RCCL without local registration,
+# and hipMalloc'd buffers.  MODE=nofill: late with decoys never written (copy
+# kernel, RCCL), and the written case again.  Stops at the first run that ends other than 0 (right) or 1 (wrong).
 #   tools/rccl_vmm_reuse.sh OUT_DIR [build]
 set -uo pipefail
 cd "$(dirname "$0")/.."
@@ -24,7 +28,15 @@ run() {  # NAME ARGS...
   echo "{\"run\": \"$name\", \"rc\": $rc}"
   [ $rc -le 1 ]
 }
-if [ "${MODE:-}" = swap ]; then
+if [ "${MODE:-}" = nofill ]; then
+  run late_kernel_nofill 4 4 2 8 late kernel nofill && run late_rccl_nofill 4 4 2 8 late rccl nofill &&
+    run late_kernel_fill 4 4 2 8 late kernel fill
+elif [ "${MODE:-}" = transport ]; then
+  run late_memcpy 4 4 2 8 late memcpy && run late_kernel 4 4 2 8 late kernel &&
+    NCCL_LOCAL_REGISTER=0 run late_noreg 4 4 2 8 late rccl && run late_malloc 4 4 2 8 malloc rccl
+elif [ "${MODE:-}" = late ]; then
+  run late_decoys2 6 4 2 8 late && run late_decoys3 6 4 3 8 late
+elif [ "${MODE:-}" = swap ]; then
   run swap_plain 6 4 0 8 swap && run swap_decoys 6 4 2 8 swap
 else
   run vmm_decoys 6 4 2 8 && run vmm_plain 6 4 0 8 && run malloc 6 4 2 8 malloc
