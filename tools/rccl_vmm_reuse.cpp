@@ -11,9 +11,11 @@
 // checked on the device; then everything released.  One JSON line per
 // iteration with the buffers' addresses and the wrong u64 count.
 //
-//   tools/rccl_vmm_reuse ITERS SIZE_GIB DECOYS ROUNDS [malloc|swap|late|vmm] [rccl|memcpy|kernel] [nofill]
+//   tools/rccl_vmm_reuse ITERS SIZE_GIB DECOYS ROUNDS [malloc|swap|late|chain|vmm] [rccl|memcpy|kernel] [nofill|nomemset]
 //   (swap: odd iterations back the reused ranges with other physical pieces;
-//    late: decoys written, released, then the receive buffer allocated)
+//    late: decoys written, released, then the receive buffer allocated;
+//    chain: the placement probe's candidates, each written, checked and
+//    released before the next is mapped)
 //
 // Build: hipcc --offload-arch=gfx950 -O2 tools/rccl_vmm_reuse.cpp -lrccl (tools/rccl_vmm_reuse.sh).
 #include <hip/hip_runtime.h>
@@ -134,7 +136,7 @@ void free_buf(Buf& b) {
 
 int main(int argc, char** argv) {
   if (argc < 5) {
-    fprintf(stderr, "usage: %s ITERS SIZE_GIB DECOYS ROUNDS [malloc|swap|late|vmm] [rccl|memcpy|kernel] [nofill]\n", argv[0]);
+    fprintf(stderr, "usage: %s ITERS SIZE_GIB DECOYS ROUNDS [malloc|swap|late|chain|vmm] [rccl|memcpy|kernel] [nofill|nomemset]\n", argv[0]);
     return 1;
   }
   const int iters = atoi(argv[1]), decoys = atoi(argv[3]), rounds = atoi(argv[4]);
@@ -142,6 +144,8 @@ int main(int argc, char** argv) {
   const bool vmm = !(argc > 5 && !strcmp(argv[5], "malloc"));
   const bool swap = argc > 5 && !strcmp(argv[5], "swap");
   const bool late = argc > 5 && !strcmp(argv[5], "late");
+  const bool chain = argc > 5 && !strcmp(argv[5], "chain");
+  const bool nomemset = argc > 7 && !strcmp(argv[7], "nomemset");  // chain: no hipMemsetAsync of a candidate
   // transport (argv[6]): rccl (default) | memcpy (hipMemcpyAsync) | kernel (a copy kernel)
   const bool nofill = argc > 7 && !strcmp(argv[7], "nofill");  // late: decoys never written
   const int transport = argc > 6 ? (!strcmp(argv[6], "memcpy") ? 1 : !strcmp(argv[6], "kernel") ? 2 : 0) : 0;
@@ -162,6 +166,37 @@ int main(int argc, char** argv) {
     CN(ncclCommInitRank(&comm, 1, id, 0));
     hipStream_t s;
     CK(hipStreamCreate(&s));
+    if (chain) {
+      // The placement probe's pattern (lsb_alloc.cpp Chain / alloc_third):
+      // candidate k is mapped, written (copy of the send buffer), checked and
+      // released, and candidate k + 1 is mapped at once -- DECOYS + 1 times.
+      Buf src = alloc_buf(bytes, vmm);
+      unsigned long long wrong = 0;
+      void* first = nullptr;
+      int same = 0;
+      for (int k = 0; k <= decoys; ++k) {
+        Buf cand = alloc_buf(bytes, vmm);
+        if (k == 0) first = cand.base;
+        else same += cand.base == first;
+        k_fill<<<4096, 256, 0, s>>>(static_cast<uint64_t*>(src.base), n, it, k);
+        if (!nomemset) CK(hipMemsetAsync(cand.base, 0, bytes, s));  // the probe never clears a candidate
+        k_copy<<<4096, 256, 0, s>>>(static_cast<uint64_t*>(cand.base), static_cast<const uint64_t*>(src.base), n);
+        CK(hipMemsetAsync(bad, 0, sizeof(unsigned long long), s));
+        k_check<<<4096, 256, 0, s>>>(static_cast<const uint64_t*>(cand.base), n, it, k, bad);
+        unsigned long long h = 0;
+        CK(hipMemcpyAsync(&h, bad, sizeof h, hipMemcpyDeviceToHost, s));
+        CK(hipStreamSynchronize(s));
+        wrong += h;
+        free_buf(cand);
+      }
+      printf("{\"iter\": %d, \"chain\": %d, \"same_address\": %d, \"wrong_u64\": %llu}\n", it, decoys + 1, same, wrong);
+      fflush(stdout);
+      if (wrong) worst = 1;
+      free_buf(src);
+      CK(hipStreamDestroy(s));
+      CN(ncclCommDestroy(comm));
+      continue;
+    }
     std::vector<Buf> decoy;
     for (int d = 0; d < decoys; ++d) decoy.push_back(alloc_buf(bytes, vmm));
     // swap: on odd iterations the ranges are backed in the other order, after

@@ -9,7 +9,9 @@
 # buffer allocated (liblsb's order), with 2 and 3 decoys.  MODE=transport:
 # late with hipMemcpyAsync, a copy kernel, RCCL without local registration,
 # and hipMalloc'd buffers.  MODE=nofill: late with decoys never written (copy
-# kernel, RCCL), and the written case again.  Stops at the first run that ends other than 0 (right) or 1 (wrong).
+# kernel, RCCL), and the written case again.  MODE=chain: the placement
+# probe's pattern (4 and 8 candidates), and late with a copy kernel again.
+# MODE=chain_nomemset: 8 candidates without and with the hipMemsetAsync.  Stops at the first run that ends other than 0 (right) or 1 (wrong).
 #   tools/rccl_vmm_reuse.sh OUT_DIR [build]
 set -uo pipefail
 cd "$(dirname "$0")/.."
@@ -28,7 +30,11 @@ run() {  # NAME ARGS...
   echo "{\"run\": \"$name\", \"rc\": $rc}"
   [ $rc -le 1 ]
 }
-if [ "${MODE:-}" = nofill ]; then
+if [ "${MODE:-}" = chain_nomemset ]; then
+  run chain8_nomemset 4 4 7 1 chain kernel nomemset && run chain8_memset 4 4 7 1 chain kernel memset
+elif [ "${MODE:-}" = chain ]; then
+  run chain4 4 4 3 1 chain && run chain8 4 4 7 1 chain && run late_kernel_again 4 4 2 8 late kernel
+elif [ "${MODE:-}" = nofill ]; then
   run late_kernel_nofill 4 4 2 8 late kernel nofill && run late_rccl_nofill 4 4 2 8 late rccl nofill &&
     run late_kernel_fill 4 4 2 8 late kernel fill
 elif [ "${MODE:-}" = transport ]; then
